@@ -1,0 +1,139 @@
+/*
+ * mcc.h -- C ABI of the MI355X multi-camera bundle-adjustment hot path (libmcc.so).
+ *
+ * Drop-in boundary for MultiCameraCalibration::optimizeExtrinsics and its per-iteration
+ * linearisation seam in the reference (yulong314/multi_camera_calibration):
+ *
+ *   mcc_create ........... replaces the problem state the reference keeps in _edgeList /
+ *                          _vertexList / _objectPointsForEachCamera / _imagePointsForEachCamera /
+ *                          _cameraMatrix / _distortCoeffs / _xi (include/opencv2/ccalib/
+ *                          multicalib.hpp:207-214, mymulticalib.hpp:122-126, doubleSide.hpp:128-130)
+ *                          once loadImages()+initialize() have built it.
+ *   mcc_linearize_solve .. replaces the virtual computeJacobianExtrinsic(x, JTJ_inv, JTE, deltaX)
+ *                          (multicalib.hpp:176 -> src/multicalib.cpp:593-703,
+ *                          mymulticalib.hpp:164 -> src/mymulticalib.cpp:668-818,
+ *                          doubleSide.hpp:133 -> src/doubleSide.cpp:434-581): one linearisation and
+ *                          the normal-equation solve; JTJ_inv is never materialised.
+ *   mcc_optimize ......... replaces the loop of optimizeExtrinsics (multicalib.hpp:155 ->
+ *                          src/multicalib.cpp:462-507): undamped Gauss-Newton with the
+ *                          0.95^(k+1) step factor and float32 state, driven on the device.
+ *   mcc_project_error .... replaces the virtual computeProjectError(x) (multicalib.hpp:188 ->
+ *                          src/multicalib.cpp:895-1006, src/mymulticalib.cpp:820-939,
+ *                          src/doubleSide.cpp:640-769): per-edge float32 error sums in reference
+ *                          order and the reference's meanReProjError.
+ *   mcc_comm_* ........... multi-GPU: photo vertices sharded over ranks, one RCCL all-reduce of the
+ *                          reduced camera system per Gauss-Newton step (no reference counterpart).
+ *
+ * Conventions: every function returns 0 on success or a negative MCC_E* code; the message is
+ * in mcc_last_error() (thread-local).  Nothing throws across the ABI.  Inputs are deep-copied
+ * to the device by mcc_create; output pointers are caller-allocated host memory.  One
+ * mcc_problem per host thread; calls on one problem are serialised by the caller (the
+ * reference is single-threaded and non-reentrant, src/multicalib.cpp:120).
+ */
+#ifndef MCC_H
+#define MCC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCC_OK 0
+#define MCC_EINVAL (-1)     /* bad argument / unsupported configuration          */
+#define MCC_EHIP (-2)       /* HIP runtime error                                 */
+#define MCC_ENOTPD (-3)     /* a normal-equation block is not positive definite  */
+#define MCC_ECOMM (-4)      /* RCCL error                                        */
+#define MCC_ENOMEM (-5)
+
+/* Camera model / class semantics the linearisation follows. */
+#define MCC_MODEL_PINHOLE 0     /* MyMultiCameraCalibration, cv::projectPoints (k1..k6,p1,p2,s1..s4) */
+#define MCC_MODEL_OMNI 1        /* MultiCameraCalibration base class, cv::omnidir::projectPoints    */
+#define MCC_MODEL_DOUBLESIDE 2  /* DoubleSideCalibration (pinhole), fixed cameras + ds transform    */
+
+#define MCC_FRONT 0             /* MultiCameraCalibration::FRONT_PATTERN (multicalib.hpp:82) */
+#define MCC_BACK 1              /* MultiCameraCalibration::BACK_PATTERN                      */
+
+/* TermCriteria types as the reference tests them (src/multicalib.cpp:475-477). */
+#define MCC_CRIT_COUNT 1
+#define MCC_CRIT_EPS 2
+#define MCC_CRIT_COUNT_EPS 3
+
+typedef struct mcc_problem mcc_problem;
+
+/* Problem description in the reference's layout.  Camera vertices 0..n_cams-1 (camera 0 is the
+ * identity and is not optimised), photo vertices n_cams.. are given as photo indices
+ * 0..n_photos-1.  Edges are in reference order (_edgeList).  Parameters follow buildParas
+ * (src/multicalib.cpp:422-440): [cam1..cam(C-1), photo0..] x (rvec, tvec), or for DOUBLESIDE
+ * (src/doubleSide.cpp:233-261): [ds, photo0..]. */
+typedef struct mcc_desc {
+    int model;
+    int n_cams, n_photos, n_edges;
+    const int *edge_cam;     /* [E] camera vertex                                  */
+    const int *edge_photo;   /* [E] photo index                                    */
+    const int *edge_side;    /* [E] MCC_FRONT / MCC_BACK (NULL = all front)        */
+    const int *edge_off;     /* [E] first corner of the edge in obj/img            */
+    const int *edge_n;       /* [E] corners of the edge                            */
+    const float *obj;        /* [3*corners] object points, float32                 */
+    const float *img;        /* [2*corners] observed corners, float32              */
+    int nd;                  /* distortion coefficients per camera: pinhole 4/5/8/12, omni 4 */
+    const float *K;          /* [9*n_cams] camera matrices (row-major), float32     */
+    const float *D;          /* [nd*n_cams] distortion, float32                    */
+    const float *xi;         /* [n_cams] Mei xi (OMNI), else NULL                  */
+    const double *ds_pose;   /* [16] PINHOLE: doubleSideTransform (CV_64F 4x4), used by BACK edges */
+    const float *cam_pose;   /* [16*n_cams] DOUBLESIDE: fixed camera poses (CV_32F 4x4)            */
+    int device;              /* HIP device ordinal                                 */
+} mcc_desc;
+
+int mcc_create(mcc_problem **out, const mcc_desc *desc);
+void mcc_destroy(mcc_problem *p);
+const char *mcc_last_error(void);
+
+int mcc_nparams(const mcc_problem *p);            /* P of this (local) problem              */
+int mcc_global_dim(const mcc_problem *p);         /* m: 6(C-1), or 6 for DOUBLESIDE         */
+
+int mcc_set_params(mcc_problem *p, const float *x, int n);
+int mcc_get_params(mcc_problem *p, float *x, int n);
+
+/* One linearisation + normal-equation solve at the current parameters (no update).
+ * delta[P], jte[P] (either may be NULL): the reference's deltaX and JTE. */
+int mcc_linearize_solve(mcc_problem *p, double *delta, double *jte);
+
+/* optimizeExtrinsics' loop (without the final computeProjectError).  x_inout[P] holds the
+ * initial float32 parameters and receives the result.  iters / last_change may be NULL. */
+int mcc_optimize(mcc_problem *p, int crit_type, int max_count, double eps, float *x_inout,
+                 int *iters, double *last_change);
+
+/* n unconditional Gauss-Newton iterations on the device-resident parameters, enqueued
+ * asynchronously (bench / throughput path).  Use mcc_synchronize to wait. */
+int mcc_step(mcc_problem *p, int n);
+int mcc_synchronize(mcc_problem *p);
+
+/* computeProjectError(x): edge_err[E] (reference edge order, may be NULL), mean. */
+int mcc_project_error(mcc_problem *p, const float *x, float *edge_err, double *mean);
+
+/* ---- multi-GPU (RCCL over xGMI).  All ranks hold the same cameras and disjoint photo sets;
+ * x of a rank is [global block, its photos].  The global block stays identical on all ranks. */
+#define MCC_UNIQUE_ID_BYTES 128
+int mcc_comm_unique_id(unsigned char *id /* [128] */);
+int mcc_comm_init(mcc_problem *p, const unsigned char *id, int nranks, int rank);
+/* greedy balance of photos over ranks by corner count (descending); rank_of_photo[n_photos] */
+int mcc_partition_photos(int n_photos, int n_edges, const int *edge_photo, const int *edge_n,
+                         int nranks, int *rank_of_photo);
+/* collective helpers on the problem's communicator (device-side, blocking) */
+int mcc_comm_allreduce_max(mcc_problem *p, double *v);
+int mcc_comm_barrier(mcc_problem *p);
+
+/* ---- diagnostics / measurement */
+/* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
+int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
+/* average device time (ms) per launch of the linearisation kernel over the last
+ * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches */
+int mcc_timing_begin(mcc_problem *p);
+int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
+/* static facts about the problem for roofline accounting */
+int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges,
+                      long long *photos, long long *alg_bytes_per_step);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

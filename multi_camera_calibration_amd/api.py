@@ -1,0 +1,246 @@
+"""Python binding of libmcc.so (include/mcc.h) -- the MI355X hot path behind the reference's
+optimiser seam.
+
+Mirrors the reference's operator interface for this path (cv::multicalib, include/opencv2/ccalib/
+multicalib.hpp:155-188):
+
+    BundleAdjuster.optimize_extrinsics(...)       -> MultiCameraCalibration::optimizeExtrinsics
+    BundleAdjuster.compute_jacobian_extrinsic(x)  -> computeJacobianExtrinsic(x, JTJ_inv, JTE, deltaX)
+    BundleAdjuster.compute_project_error(x)       -> computeProjectError(x)
+
+There is no CPU fallback: if libmcc.so is missing or the device is unusable the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+from . import rig as _rig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmcc.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "mcc.h")
+
+_i32p = ctypes.POINTER(ctypes.c_int)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+MCC_CRIT_COUNT, MCC_CRIT_EPS, MCC_CRIT_COUNT_EPS = 1, 2, 3
+
+
+class MccError(RuntimeError):
+    pass
+
+
+class _Desc(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int), ("n_cams", ctypes.c_int), ("n_photos", ctypes.c_int),
+                ("n_edges", ctypes.c_int), ("edge_cam", _i32p), ("edge_photo", _i32p),
+                ("edge_side", _i32p), ("edge_off", _i32p), ("edge_n", _i32p),
+                ("obj", _f32p), ("img", _f32p), ("nd", ctypes.c_int), ("K", _f32p),
+                ("D", _f32p), ("xi", _f32p), ("ds_pose", _f64p), ("cam_pose", _f32p),
+                ("device", ctypes.c_int)]
+
+
+_LIB = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libmcc.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    srcs = [os.path.join(_HERE, "csrc", f) for f in os.listdir(os.path.join(_HERE, "csrc"))]
+    srcs.append(HEADER)
+    stale = not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs)
+    if force or stale:
+        subprocess.run(["make", "-C", _HERE, "-j4", "libmcc.so"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise MccError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.mcc_last_error.restype = ctypes.c_char_p
+        L.mcc_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_Desc)]
+        for name in ("mcc_nparams", "mcc_global_dim"):
+            getattr(L, name).argtypes = [ctypes.c_void_p]
+        L.mcc_destroy.argtypes = [ctypes.c_void_p]
+        L.mcc_destroy.restype = None
+        L.mcc_set_params.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int]
+        L.mcc_get_params.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int]
+        L.mcc_linearize_solve.argtypes = [ctypes.c_void_p, _f64p, _f64p]
+        L.mcc_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, _f32p,
+                                   _i32p, _f64p]
+        L.mcc_step.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.mcc_synchronize.argtypes = [ctypes.c_void_p]
+        L.mcc_project_error.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f64p]
+        L.mcc_debug_residuals.argtypes = [ctypes.c_void_p, _f32p, _f32p]
+        L.mcc_timing_begin.argtypes = [ctypes.c_void_p]
+        L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
+        L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
+        L.mcc_comm_unique_id.argtypes = [ctypes.c_char_p]
+        L.mcc_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.mcc_comm_allreduce_max.argtypes = [ctypes.c_void_p, _f64p]
+        L.mcc_comm_barrier.argtypes = [ctypes.c_void_p]
+        L.mcc_partition_photos.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p]
+        _LIB = L
+    return _LIB
+
+
+def declared_symbols():
+    """Every function include/mcc.h declares."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(mcc_[a-z_]+)\s*\(", txt, re.M)))
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise MccError(f"{what} failed ({rc}): {lib().mcc_last_error().decode()}")
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def partition_photos(prob, nranks):
+    """Greedy corner-count balance of photo vertices over ranks (mcc_partition_photos)."""
+    out = np.zeros(prob.n_photos, np.int32)
+    ep = np.ascontiguousarray(prob.edge_photo, np.int32)
+    en = np.ascontiguousarray(prob.edge_n, np.int32)
+    _check(lib().mcc_partition_photos(prob.n_photos, prob.n_edges, _ptr(ep, _i32p), _ptr(en, _i32p),
+                                      nranks, _ptr(out, _i32p)), "mcc_partition_photos")
+    return out
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().mcc_comm_unique_id(buf), "mcc_comm_unique_id")
+    return buf.raw
+
+
+class BundleAdjuster:
+    """One mcc_problem: the reference's BA state for one (local) set of photo vertices."""
+
+    def __init__(self, prob: "_rig.Problem", device: int = 0):
+        self.prob = prob
+        self._keep = []
+
+        def arr(a, dt):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, dtype=dt)
+            self._keep.append(a)
+            return a
+        d = _Desc()
+        d.model, d.n_cams, d.n_photos, d.n_edges = prob.model, prob.n_cams, prob.n_photos, prob.n_edges
+        d.edge_cam = _ptr(arr(prob.edge_cam, np.int32), _i32p)
+        d.edge_photo = _ptr(arr(prob.edge_photo, np.int32), _i32p)
+        d.edge_side = _ptr(arr(prob.edge_side, np.int32), _i32p)
+        d.edge_off = _ptr(arr(prob.edge_off, np.int32), _i32p)
+        d.edge_n = _ptr(arr(prob.edge_n, np.int32), _i32p)
+        d.obj = _ptr(arr(prob.obj, np.float32), _f32p)
+        d.img = _ptr(arr(prob.img, np.float32), _f32p)
+        d.nd = prob.nd
+        d.K = _ptr(arr(prob.K, np.float32), _f32p)
+        d.D = _ptr(arr(prob.D, np.float32), _f32p)
+        d.xi = _ptr(arr(prob.xi, np.float32), _f32p) if prob.model == _rig.OMNI else None
+        d.ds_pose = _ptr(arr(prob.ds_pose, np.float64), _f64p) if prob.ds_pose is not None else None
+        d.cam_pose = _ptr(arr(prob.cam_pose, np.float32), _f32p) if prob.cam_pose is not None else None
+        d.device = device
+        h = ctypes.c_void_p()
+        _check(lib().mcc_create(ctypes.byref(h), ctypes.byref(d)), "mcc_create")
+        self.h = h
+        self.P = lib().mcc_nparams(h)
+        self.m = lib().mcc_global_dim(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mcc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- state
+    def set_params(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        _check(lib().mcc_set_params(self.h, _ptr(x, _f32p), x.size), "mcc_set_params")
+
+    def get_params(self):
+        x = np.zeros(self.P, np.float32)
+        _check(lib().mcc_get_params(self.h, _ptr(x, _f32p), self.P), "mcc_get_params")
+        return x
+
+    # -- the reference seam
+    def compute_jacobian_extrinsic(self, x):
+        """(deltaX, JTE) of one linearisation at x (computeJacobianExtrinsic)."""
+        self.set_params(x)
+        delta = np.zeros(self.P)
+        jte = np.zeros(self.P)
+        _check(lib().mcc_linearize_solve(self.h, _ptr(delta, _f64p), _ptr(jte, _f64p)), "mcc_linearize_solve")
+        return delta, jte
+
+    def optimize_extrinsics(self, x0, crit_type=MCC_CRIT_COUNT_EPS, max_count=200, eps=1e-7):
+        """optimizeExtrinsics: returns (x, meanReProjError, iterations, last change)."""
+        x = np.array(x0, np.float32, copy=True)
+        it = ctypes.c_int(0)
+        ch = ctypes.c_double(0)
+        _check(lib().mcc_optimize(self.h, crit_type, max_count, eps, _ptr(x, _f32p), ctypes.byref(it),
+                                  ctypes.byref(ch)), "mcc_optimize")
+        _, mean = self.compute_project_error(x)
+        return x, mean, it.value, ch.value
+
+    def compute_project_error(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        err = np.zeros(self.prob.n_edges, np.float32)
+        mean = ctypes.c_double(0)
+        _check(lib().mcc_project_error(self.h, _ptr(x, _f32p), _ptr(err, _f32p), ctypes.byref(mean)),
+               "mcc_project_error")
+        return err, mean.value
+
+    # -- throughput path
+    def step(self, n):
+        _check(lib().mcc_step(self.h, n), "mcc_step")
+
+    def synchronize(self):
+        _check(lib().mcc_synchronize(self.h), "mcc_synchronize")
+
+    def residuals(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        r = np.zeros(2 * self.prob.n_corners, np.float32)
+        _check(lib().mcc_debug_residuals(self.h, _ptr(x, _f32p), _ptr(r, _f32p)), "mcc_debug_residuals")
+        return r
+
+    def timing_begin(self):
+        _check(lib().mcc_timing_begin(self.h), "mcc_timing_begin")
+
+    def timing_end(self):
+        lin = ctypes.c_double(0)
+        st = ctypes.c_double(0)
+        n = ctypes.c_int(0)
+        _check(lib().mcc_timing_end(self.h, ctypes.byref(lin), ctypes.byref(st), ctypes.byref(n)), "mcc_timing_end")
+        return lin.value, st.value, n.value
+
+    def stats(self):
+        v = [ctypes.c_longlong(0) for _ in range(4)]
+        _check(lib().mcc_problem_stats(self.h, *[ctypes.byref(t) for t in v]), "mcc_problem_stats")
+        return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
+
+    # -- multi-GPU
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        _check(lib().mcc_comm_init(self.h, uid, nranks, rank), "mcc_comm_init")
+
+    def allreduce_max(self, v: float) -> float:
+        d = ctypes.c_double(v)
+        _check(lib().mcc_comm_allreduce_max(self.h, ctypes.byref(d)), "mcc_comm_allreduce_max")
+        return d.value
+
+    def barrier(self):
+        _check(lib().mcc_comm_barrier(self.h), "mcc_comm_barrier")

@@ -1,0 +1,710 @@
+// mcc_api.cpp -- host side of libmcc.so: the extern "C" ABI of include/mcc.h.
+//
+// mcc_create turns the reference's problem (edge list + per-edge corner Mats + intrinsics, as
+// MyMultiCameraCalibration::loadImages/initialize leave them, src/mymulticalib.cpp:348-405,
+// 615-667) into a photo-major, structure-of-arrays layout in HBM, precomputes the Schur pair
+// lists, and drives the Gauss-Newton loop of optimizeExtrinsics (src/multicalib.cpp:462-514)
+// on one HIP stream, captured as hipGraphs.  Multi-GPU: one process per GPU, photo vertices
+// sharded, one RCCL all-reduce of the packed reduced camera system per step.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/mcc.h"
+#include "mcc_internal.h"
+
+using mcc::State;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return fail(MCC_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    hipError_t alloc(size_t count) {
+        n = count;
+        return hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+    }
+    hipError_t upload(const T* h, size_t count) {
+        hipError_t e = alloc(count);
+        if (e != hipSuccess) return e;
+        if (count) e = hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
+};
+
+// Host restatement of cvRodrigues2 matrix -> vector (with the polar re-orthonormalisation)
+// used once per problem for fixed transforms (doubleSideTransform2vec,
+// src/mymulticalib.cpp:105-117; cameraPose2vec, src/doubleSide.cpp:262-275).
+void host_rodrigues_m2v(const double* Rin, double* r) {
+    double R[9];
+    std::memcpy(R, Rin, sizeof(R));
+    for (int it = 0; it < 40; ++it) {
+        double cof[9] = {R[4] * R[8] - R[5] * R[7], -(R[3] * R[8] - R[5] * R[6]), R[3] * R[7] - R[4] * R[6],
+                         -(R[1] * R[8] - R[2] * R[7]), R[0] * R[8] - R[2] * R[6], -(R[0] * R[7] - R[1] * R[6]),
+                         R[1] * R[5] - R[2] * R[4], -(R[0] * R[5] - R[2] * R[3]), R[0] * R[4] - R[1] * R[3]};
+        double d = R[0] * cof[0] + R[1] * cof[1] + R[2] * cof[2], delta = 0;
+        if (!(std::fabs(d) > 1e-300)) break;
+        for (int k = 0; k < 9; ++k) {
+            double v = 0.5 * (R[k] + cof[k] / d);
+            delta = std::max(delta, std::fabs(v - R[k]));
+            R[k] = v;
+        }
+        if (delta < 1e-15) break;
+    }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double theta = std::acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t;
+            t = (R[0] + 1) * 0.5; rx = std::sqrt(std::max(t, 0.));
+            t = (R[4] + 1) * 0.5; ry = std::sqrt(std::max(t, 0.)) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5; rz = std::sqrt(std::max(t, 0.)) * (R[2] < 0 ? -1. : 1.);
+            if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            theta /= std::sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= theta; ry *= theta; rz *= theta;
+        }
+    } else {
+        double vth = 1 / (2 * s) * theta;
+        rx *= vth; ry *= vth; rz *= vth;
+    }
+    r[0] = rx; r[1] = ry; r[2] = rz;
+}
+
+}  // namespace
+
+struct mcc_problem {
+    int model = 0, C = 0, V = 0, E = 0, nd = 0, m = 0, P = 0, device = 0;
+    long long corners = 0;
+    bool rational = false, prism = false;
+    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0;
+    hipStream_t stream = nullptr;
+
+    // host-side maps
+    std::vector<int> dev2ref_edge;      // device edge -> reference edge
+    std::vector<long long> dev2ref_corner;
+    std::vector<int> edge_n_dev;
+
+    // device buffers
+    DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
+    DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha;
+    DevBuf<int> photo_ptr, edge_gblock, block_items, gblock_ptr, gblock_edges, edge_photo;
+    DevBuf<int4> edge_info, items, pairs;
+    DevBuf<State> state;
+    State* h_state = nullptr;   // pinned staging
+    int packed_len = 0, ntri = 0;
+
+    // graphs: [0] one update step, [1] kGraphSteps update steps
+    static constexpr int kGraphSteps = 8;
+    hipGraphExec_t gexec[2] = {nullptr, nullptr};
+    bool use_graph = true;
+
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+
+    // timing window
+    bool timing = false;
+    std::vector<hipEvent_t> ev_lin, ev_step;
+    int ev_used = 0;
+};
+
+namespace {
+
+int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
+    using namespace mcc;
+    const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
+    if (tim) HIPCHK(hipEventRecord(p->ev_step[p->ev_used], p->stream));
+    if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used], p->stream));
+    LinArgs la{};
+    la.state = p->state.p;
+    la.photo_ptr = p->photo_ptr.p;
+    la.edge_info = p->edge_info.p;
+    la.obj_x = p->obj_x.p; la.obj_y = p->obj_y.p; la.obj_z = p->obj_z.p;
+    la.img_u = p->img_u.p; la.img_v = p->img_v.p;
+    la.x = p->x.p;
+    la.K = p->K.p; la.D = p->D.p; la.xi = p->xi.p;
+    la.cam_rt = p->cam_rt.p; la.ds_rt = p->ds_rt.p;
+    la.nd = p->nd; la.global_dim = p->m;
+    la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.gg = p->gg.p; la.Lp = p->Lp.p; la.zp = p->zp.p;
+    la.gp_tot = p->gp_tot.p;
+    la.resid = resid_dev;
+    if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
+    if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
+
+    SchurArgs sa{p->state.p, p->items.p, p->pairs.p, p->Y.p, p->Hgg.p, p->gg.p, p->zp.p, p->item_out.p};
+    HIPCHK(mcc_launch_schur(sa, p->n_items, p->stream));
+    AsmArgs aa{p->state.p, p->block_items.p, p->item_out.p, p->gblock_ptr.p, p->gblock_edges.p, p->gg.p,
+               p->photo_norm.p, p->packed.p, p->m, p->V, p->rank};
+    HIPCHK(mcc_launch_assemble(aa, p->stream));
+    if (p->comm && p->nranks > 1) {
+        ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
+                                       p->comm, p->stream);
+        if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
+    SolveArgs so{p->state.p, p->packed.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+    HIPCHK(mcc_launch_solve(so, p->stream));
+    BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->Lp.p, p->zp.p, p->dg.p,
+                   p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
+    HIPCHK(mcc_launch_backsub(ba, p->stream));
+    if (tim) {
+        HIPCHK(hipEventRecord(p->ev_step[p->ev_used + 1], p->stream));
+        p->ev_used += 2;
+    }
+    return MCC_OK;
+}
+
+int build_graphs(mcc_problem* p) {
+    if (p->gexec[0]) return MCC_OK;
+    const int counts[2] = {1, mcc_problem::kGraphSteps};
+    for (int g = 0; g < 2; ++g) {
+        hipGraph_t graph;
+        HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+        int rc = MCC_OK;
+        for (int s = 0; s < counts[g] && rc == MCC_OK; ++s) rc = enqueue_step(p, 1, nullptr);
+        hipError_t ee = hipStreamEndCapture(p->stream, &graph);
+        if (rc != MCC_OK) return rc;
+        if (ee != hipSuccess) return fail(MCC_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ee));
+        HIPCHK(hipGraphInstantiate(&p->gexec[g], graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(graph));
+    }
+    return MCC_OK;
+}
+
+int launch_update_steps(mcc_problem* p, int n) {
+    if (p->timing || !p->use_graph) {
+        for (int i = 0; i < n; ++i) {
+            int rc = enqueue_step(p, 1, nullptr);
+            if (rc) return rc;
+        }
+        return MCC_OK;
+    }
+    int rc = build_graphs(p);
+    if (rc) return rc;
+    while (n >= mcc_problem::kGraphSteps) {
+        HIPCHK(hipGraphLaunch(p->gexec[1], p->stream));
+        n -= mcc_problem::kGraphSteps;
+    }
+    while (n-- > 0) HIPCHK(hipGraphLaunch(p->gexec[0], p->stream));
+    return MCC_OK;
+}
+
+int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, double eps) {
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
+    if (reset_iter) {
+        p->h_state->iter = 0;
+        p->h_state->change = 1.0;
+        p->h_state->cam_normG2 = p->h_state->cam_normX2 = 0.0;
+    }
+    p->h_state->done = 0;
+    p->h_state->crit_type = crit_type;
+    p->h_state->max_count = max_count;
+    p->h_state->eps = eps;
+    p->h_state->error = 0;
+    HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
+    return MCC_OK;
+}
+
+int read_state(mcc_problem* p) {
+    HIPCHK(hipMemcpyAsync(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    return MCC_OK;
+}
+
+int check_state_error(mcc_problem* p) {
+    if (p->h_state->error & 2) return fail(MCC_ENOTPD, "reduced camera system is not positive definite");
+    if (p->h_state->error & 1) return fail(MCC_ENOTPD, "a photo normal-equation block is not positive definite");
+    return MCC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mcc_last_error(void) { return g_err.c_str(); }
+
+int mcc_nparams(const mcc_problem* p) { return p ? p->P : 0; }
+int mcc_global_dim(const mcc_problem* p) { return p ? p->m : 0; }
+
+int mcc_create(mcc_problem** out, const mcc_desc* d) {
+    if (!out || !d) return fail(MCC_EINVAL, "null argument");
+    *out = nullptr;
+    if (d->model < 0 || d->model > 2) return fail(MCC_EINVAL, "unknown model");
+    if (d->n_cams < 1 || d->n_photos < 0 || d->n_edges < 0) return fail(MCC_EINVAL, "bad sizes");
+    if (d->model != MCC_MODEL_DOUBLESIDE && d->n_cams < 2) return fail(MCC_EINVAL, "need >= 2 cameras");
+    if (d->model == MCC_MODEL_OMNI && (d->nd != 4 || !d->xi)) return fail(MCC_EINVAL, "omni needs nd == 4 and xi");
+    if (d->model != MCC_MODEL_OMNI && !(d->nd == 4 || d->nd == 5 || d->nd == 8 || d->nd == 12 || d->nd == 14))
+        return fail(MCC_EINVAL, "pinhole nd must be 4, 5, 8, 12 or 14");
+    if (d->model == MCC_MODEL_DOUBLESIDE && !d->cam_pose) return fail(MCC_EINVAL, "DOUBLESIDE needs cam_pose");
+    const int C = d->n_cams, V = d->n_photos, E = d->n_edges;
+    for (int e = 0; e < E; ++e) {
+        if (d->edge_cam[e] < 0 || d->edge_cam[e] >= C || d->edge_photo[e] < 0 || d->edge_photo[e] >= V ||
+            d->edge_n[e] < 1 || d->edge_off[e] < 0)
+            return fail(MCC_EINVAL, "edge " + std::to_string(e) + " out of range");
+        if (d->edge_n[e] > 1024) return fail(MCC_EINVAL, "more than 1024 corners in an edge");
+        int side = d->edge_side ? d->edge_side[e] : MCC_FRONT;
+        if (side == MCC_BACK && d->model == MCC_MODEL_PINHOLE && !d->ds_pose)
+            return fail(MCC_EINVAL, "BACK edge without doubleSideTransform (the reference dereferences an empty Mat)");
+        if (side == MCC_BACK && d->model == MCC_MODEL_OMNI) return fail(MCC_EINVAL, "BACK edges are pinhole only");
+    }
+    for (int c = 0; c < C && d->model != MCC_MODEL_OMNI; ++c)
+        if (d->nd == 14 && (d->D[14 * c + 12] != 0.f || d->D[14 * c + 13] != 0.f))
+            return fail(MCC_EINVAL, "tilted-sensor distortion (tau_x, tau_y != 0) is not supported");
+
+    mcc_problem* p = new mcc_problem();
+    p->model = d->model; p->C = C; p->V = V; p->E = E; p->nd = d->nd; p->device = d->device;
+    p->m = d->model == MCC_MODEL_DOUBLESIDE ? 6 : 6 * (C - 1);
+    p->P = p->m + 6 * V;
+    int rc = MCC_OK;
+    auto bail = [&](int code) { mcc_destroy(p); return code; };
+#define HIPC(expr)                                                                          \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return bail(fail(MCC_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e))); \
+    } while (0)
+    HIPC(hipSetDevice(d->device));
+    HIPC(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    if (const char* g = std::getenv("MCC_GRAPH")) p->use_graph = std::atoi(g) != 0;
+
+    // distortion specialisation (zero coefficients are exact no-ops in OpenCV's formula)
+    if (d->model != MCC_MODEL_OMNI) {
+        for (int c = 0; c < C; ++c)
+            for (int q = 5; q < std::min(d->nd, 12); ++q) {
+                const float v = d->D[d->nd * c + q];
+                if (v != 0.f) (q < 8 ? p->rational : p->prism) = true;
+            }
+    }
+
+    // ---- photo-major edge order (stable within a photo: reference edge order)
+    std::vector<int> order(E);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return d->edge_photo[a] < d->edge_photo[b]; });
+    p->dev2ref_edge = order;
+    std::vector<int> photo_ptr(V + 1, 0);
+    for (int e = 0; e < E; ++e) photo_ptr[d->edge_photo[e] + 1]++;
+    for (int v = 0; v < V; ++v) {
+        p->max_epp = std::max(p->max_epp, photo_ptr[v + 1]);
+        photo_ptr[v + 1] += photo_ptr[v];
+    }
+    long long ncorner = 0;
+    for (int e = 0; e < E; ++e) ncorner += d->edge_n[e];
+    p->corners = ncorner;
+    std::vector<float> ox(ncorner), oy(ncorner), oz(ncorner), iu(ncorner), iv(ncorner);
+    std::vector<int4> info(E);
+    std::vector<int> gblock(E), ephoto(E);
+    p->dev2ref_corner.resize(ncorner);
+    p->edge_n_dev.resize(E);
+    long long off = 0;
+    for (int de = 0; de < E; ++de) {
+        const int e = order[de], n = d->edge_n[e];
+        const int side = d->edge_side ? d->edge_side[e] : MCC_FRONT;
+        for (int i = 0; i < n; ++i) {
+            const long long s = (long long)d->edge_off[e] + i;
+            ox[off + i] = d->obj[3 * s]; oy[off + i] = d->obj[3 * s + 1]; oz[off + i] = d->obj[3 * s + 2];
+            iu[off + i] = d->img[2 * s]; iv[off + i] = d->img[2 * s + 1];
+            p->dev2ref_corner[off + i] = s;
+        }
+        info[de] = make_int4(d->edge_cam[e], side, (int)off, n);
+        ephoto[de] = d->edge_photo[e];
+        p->edge_n_dev[de] = n;
+        if (d->model == MCC_MODEL_DOUBLESIDE) gblock[de] = side == MCC_BACK ? 0 : -1;
+        else gblock[de] = d->edge_cam[e] - 1;
+        off += n;
+    }
+
+    // ---- Schur pair lists grouped by camera-pair block, chunked into work items
+    const int nb = p->m / 6;
+    p->nblk = nb * (nb + 1) / 2;
+    auto blk_index = [nb](int b1, int b2) { return b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1); };
+    std::vector<std::vector<int4>> blk_pairs(p->nblk);
+    for (int v = 0; v < V; ++v)
+        for (int e1 = photo_ptr[v]; e1 < photo_ptr[v + 1]; ++e1) {
+            if (gblock[e1] < 0) continue;
+            for (int e2 = photo_ptr[v]; e2 < photo_ptr[v + 1]; ++e2) {
+                if (gblock[e2] < 0 || gblock[e1] > gblock[e2]) continue;
+                blk_pairs[blk_index(gblock[e1], gblock[e2])].push_back(make_int4(e1, e2, v, e1 == e2 ? 1 : 0));
+            }
+        }
+    std::vector<int4> pairs, items;
+    std::vector<int> block_items(p->nblk + 1, 0);
+    const int kItemPairs = 192;
+    for (int b = 0; b < p->nblk; ++b) {
+        const int begin = (int)pairs.size();
+        pairs.insert(pairs.end(), blk_pairs[b].begin(), blk_pairs[b].end());
+        const int end = (int)pairs.size();
+        for (int s = begin; s < end; s += kItemPairs) items.push_back(make_int4(b, s, std::min(end, s + kItemPairs), 0));
+        block_items[b + 1] = (int)items.size();
+    }
+    for (int b1 = 0; b1 < nb; ++b1)
+        if (blk_pairs[blk_index(b1, b1)].empty())
+            return bail(fail(MCC_EINVAL, "global block " + std::to_string(b1) + " has no observations"));
+    p->n_items = (int)items.size();
+    p->n_pairs = (int)pairs.size();
+    std::vector<int> gptr(nb + 1, 0), gedges;
+    for (int b = 0; b < nb; ++b) {
+        for (int e = 0; e < E; ++e)
+            if (gblock[e] == b) gedges.push_back(e);
+        gptr[b + 1] = (int)gedges.size();
+    }
+
+    // ---- fixed transforms
+    std::vector<float> cam_rt(6 * C, 0.f);
+    if (d->model == MCC_MODEL_DOUBLESIDE) {
+        for (int c = 0; c < C; ++c) {
+            double R[9], r[3];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) R[i * 3 + j] = d->cam_pose[16 * c + i * 4 + j];
+            host_rodrigues_m2v(R, r);
+            for (int i = 0; i < 3; ++i) { cam_rt[6 * c + i] = (float)r[i]; cam_rt[6 * c + 3 + i] = d->cam_pose[16 * c + i * 4 + 3]; }
+        }
+    }
+    double ds_rt[6] = {0, 0, 0, 0, 0, 0};
+    if (d->ds_pose && d->model == MCC_MODEL_PINHOLE) {
+        double R[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[i * 3 + j] = d->ds_pose[i * 4 + j];
+        host_rodrigues_m2v(R, ds_rt);
+        for (int i = 0; i < 3; ++i) ds_rt[3 + i] = d->ds_pose[i * 4 + 3];
+    }
+    std::vector<double> alpha(4096);
+    for (size_t k = 0; k < alpha.size(); ++k) alpha[k] = std::pow(0.95, (double)k + 1.0);   // src/multicalib.cpp:483
+
+    // ---- uploads
+    HIPC(p->obj_x.upload(ox.data(), ncorner)); HIPC(p->obj_y.upload(oy.data(), ncorner));
+    HIPC(p->obj_z.upload(oz.data(), ncorner));
+    HIPC(p->img_u.upload(iu.data(), ncorner)); HIPC(p->img_v.upload(iv.data(), ncorner));
+    HIPC(p->edge_info.upload(info.data(), E));
+    HIPC(p->edge_gblock.upload(gblock.data(), E));
+    HIPC(p->edge_photo.upload(ephoto.data(), E));
+    HIPC(p->photo_ptr.upload(photo_ptr.data(), V + 1));
+    HIPC(p->K.upload(d->K, 9 * C));
+    HIPC(p->D.upload(d->D, (size_t)d->nd * C));
+    std::vector<float> xi(C, 0.f);
+    if (d->xi) std::copy(d->xi, d->xi + C, xi.begin());
+    HIPC(p->xi.upload(xi.data(), C));
+    HIPC(p->cam_rt.upload(cam_rt.data(), 6 * C));
+    std::vector<float> cp(16 * C, 0.f);
+    if (d->cam_pose) std::copy(d->cam_pose, d->cam_pose + 16 * C, cp.begin());
+    HIPC(p->cam_pose.upload(cp.data(), 16 * C));
+    HIPC(p->ds_rt.upload(ds_rt, 6));
+    HIPC(p->alpha.upload(alpha.data(), alpha.size()));
+    HIPC(p->pairs.upload(pairs.data(), pairs.size()));
+    HIPC(p->items.upload(items.data(), items.size()));
+    HIPC(p->block_items.upload(block_items.data(), block_items.size()));
+    HIPC(p->gblock_ptr.upload(gptr.data(), gptr.size()));
+    HIPC(p->gblock_edges.upload(gedges.data(), gedges.size()));
+    HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
+    HIPC(p->Y.alloc(36 * (size_t)E)); HIPC(p->Hgg.alloc(36 * (size_t)E)); HIPC(p->gg.alloc(6 * (size_t)E));
+    HIPC(p->Lp.alloc(36 * (size_t)V)); HIPC(p->zp.alloc(6 * (size_t)V)); HIPC(p->gp_tot.alloc(6 * (size_t)V));
+    HIPC(p->item_out.alloc(42 * (size_t)items.size()));
+    p->ntri = p->m * (p->m + 1) / 2;
+    p->packed_len = p->ntri + 2 * p->m + 2;
+    HIPC(p->packed.alloc(p->packed_len));
+    HIPC(p->dg.alloc(p->m)); HIPC(p->delta.alloc(p->P));
+    HIPC(p->photo_norm.alloc(2 * (size_t)V));
+    HIPC(hipMemset(p->photo_norm.p, 0, sizeof(double) * 2 * std::max(V, 1)));
+    HIPC(p->edge_sum.alloc(E));
+    HIPC(p->state.alloc(1));
+    HIPC(hipHostMalloc((void**)&p->h_state, sizeof(State), hipHostMallocDefault));
+    std::memset(p->h_state, 0, sizeof(State));
+    p->h_state->change = 1.0;
+    HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
+    HIPC(mcc_set_lin_attrs(p->max_epp));
+    if (mcc_lin_shmem(p->max_epp) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
+#undef HIPC
+    (void)rc;
+    *out = p;
+    return MCC_OK;
+}
+
+void mcc_destroy(mcc_problem* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    for (auto& g : p->gexec)
+        if (g) (void)hipGraphExecDestroy(g);
+    for (auto e : p->ev_lin) (void)hipEventDestroy(e);
+    for (auto e : p->ev_step) (void)hipEventDestroy(e);
+    if (p->comm) (void)ncclCommDestroy(p->comm);
+    p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
+    p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
+    p->cam_pose.release(); p->resid.release(); p->edge_sum.release();
+    p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Lp.release(); p->zp.release();
+    p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
+    p->photo_norm.release(); p->alpha.release();
+    p->photo_ptr.release(); p->edge_gblock.release(); p->block_items.release(); p->gblock_ptr.release();
+    p->gblock_edges.release(); p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
+    p->state.release();
+    if (p->h_state) (void)hipHostFree(p->h_state);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+int mcc_set_params(mcc_problem* p, const float* x, int n) {
+    if (!p || !x || n != p->P) return fail(MCC_EINVAL, "mcc_set_params: size mismatch");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(p->x.p, x, sizeof(float) * n, hipMemcpyHostToDevice));
+    return MCC_OK;
+}
+
+int mcc_get_params(mcc_problem* p, float* x, int n) {
+    if (!p || !x || n != p->P) return fail(MCC_EINVAL, "mcc_get_params: size mismatch");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(x, p->x.p, sizeof(float) * n, hipMemcpyDeviceToHost));
+    return MCC_OK;
+}
+
+int mcc_linearize_solve(mcc_problem* p, double* delta, double* jte) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = set_state(p, 0, 0, 0, 0.0);
+    if (rc) return rc;
+    rc = enqueue_step(p, 0, nullptr);
+    if (rc) return rc;
+    if ((rc = read_state(p))) return rc;
+    if ((rc = check_state_error(p))) return rc;
+    if (delta) HIPCHK(hipMemcpy(delta, p->delta.p, sizeof(double) * p->P, hipMemcpyDeviceToHost));
+    if (jte) {
+        std::vector<double> pk(p->packed_len), gp(6 * (size_t)p->V);
+        HIPCHK(hipMemcpy(pk.data(), p->packed.p, sizeof(double) * p->packed_len, hipMemcpyDeviceToHost));
+        if (p->V) HIPCHK(hipMemcpy(gp.data(), p->gp_tot.p, sizeof(double) * 6 * p->V, hipMemcpyDeviceToHost));
+        for (int i = 0; i < p->m; ++i) jte[i] = pk[p->ntri + p->m + i];
+        for (int i = 0; i < 6 * p->V; ++i) jte[p->m + i] = gp[i];
+    }
+    return MCC_OK;
+}
+
+int mcc_optimize(mcc_problem* p, int crit_type, int max_count, double eps, float* x_inout, int* iters,
+                 double* last_change) {
+    if (!p || !x_inout) return fail(MCC_EINVAL, "null argument");
+    if (crit_type < 1 || crit_type > 3) return fail(MCC_EINVAL, "crit_type must be 1, 2 or 3");
+    int rc = mcc_set_params(p, x_inout, p->P);
+    if (rc) return rc;
+    if ((rc = set_state(p, 1, crit_type, max_count, eps))) return rc;
+    const long long cap = crit_type == MCC_CRIT_EPS ? 1000000LL : (long long)max_count + 1;
+    long long launched = 0;
+    while (true) {
+        const int chunk = mcc_problem::kGraphSteps;
+        if ((rc = launch_update_steps(p, chunk))) return rc;
+        launched += chunk;
+        if ((rc = read_state(p))) return rc;
+        if ((rc = check_state_error(p))) return rc;
+        if (p->h_state->done) break;
+        if (launched > cap + chunk) return fail(MCC_EINVAL, "optimize did not terminate");
+    }
+    if (iters) *iters = p->h_state->iter;
+    if (last_change) *last_change = p->h_state->change;
+    return mcc_get_params(p, x_inout, p->P);
+}
+
+int mcc_step(mcc_problem* p, int n) {
+    if (!p || n < 0) return fail(MCC_EINVAL, "bad argument");
+    HIPCHK(hipSetDevice(p->device));
+    // crit_type 0: every step updates (no stop test), iteration counter keeps running
+    int rc = set_state(p, 0, 0, 0, 0.0);
+    if (rc) return rc;
+    return launch_update_steps(p, n);
+}
+
+int mcc_synchronize(mcc_problem* p) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipStreamSynchronize(p->stream));
+    return MCC_OK;
+}
+
+int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* mean) {
+    if (!p || !x) return fail(MCC_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(p->xerr.p, x, sizeof(float) * p->P, hipMemcpyHostToDevice));
+    mcc::ErrArgs a{p->edge_info.p, p->edge_photo.p, p->obj_x.p, p->obj_y.p, p->obj_z.p, p->img_u.p, p->img_v.p,
+                   p->xerr.p, p->K.p, p->D.p, p->xi.p, p->cam_pose.p, p->edge_sum.p, p->nd, p->m};
+    if (p->E) HIPCHK(mcc_launch_project_error(a, p->model, p->E, p->rational, p->prism, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    std::vector<float> sums(p->E);
+    if (p->E) HIPCHK(hipMemcpy(sums.data(), p->edge_sum.p, sizeof(float) * p->E, hipMemcpyDeviceToHost));
+    std::vector<float> by_ref(p->E);
+    std::vector<int> n_ref(p->E);
+    for (int de = 0; de < p->E; ++de) {
+        by_ref[p->dev2ref_edge[de]] = sums[de];
+        n_ref[p->dev2ref_edge[de]] = p->edge_n_dev[de];
+    }
+    // totals in reference edge order, float32 (src/mymulticalib.cpp:913-923, hazard H6)
+    float total = 0.f;
+    long long npts = 0;
+    for (int e = 0; e < p->E; ++e) {
+        if (edge_err) edge_err[e] = by_ref[e] / n_ref[e];
+        total += by_ref[e];
+        npts += p->model == MCC_MODEL_OMNI ? n_ref[e] : 2LL * n_ref[e];   // error.total() (H2)
+    }
+    if (mean) *mean = npts ? (double)total / (double)npts : 0.0;
+    return MCC_OK;
+}
+
+int mcc_debug_residuals(mcc_problem* p, const float* x, float* res) {
+    if (!p || !x || !res) return fail(MCC_EINVAL, "null argument");
+    int rc = mcc_set_params(p, x, p->P);
+    if (rc) return rc;
+    if (!p->resid.p) HIPCHK(p->resid.alloc(2 * (size_t)std::max<long long>(p->corners, 1)));
+    if ((rc = set_state(p, 0, 0, 0, 0.0))) return rc;
+    if ((rc = enqueue_step(p, 0, p->resid.p))) return rc;
+    HIPCHK(hipStreamSynchronize(p->stream));
+    std::vector<float> r(2 * (size_t)p->corners);
+    if (p->corners) HIPCHK(hipMemcpy(r.data(), p->resid.p, sizeof(float) * r.size(), hipMemcpyDeviceToHost));
+    for (long long c = 0; c < p->corners; ++c) {
+        res[2 * p->dev2ref_corner[c]] = r[2 * c];
+        res[2 * p->dev2ref_corner[c] + 1] = r[2 * c + 1];
+    }
+    return MCC_OK;
+}
+
+int mcc_timing_begin(mcc_problem* p) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipSetDevice(p->device));
+    if (p->ev_lin.empty()) {
+        p->ev_lin.resize(512);
+        p->ev_step.resize(512);
+        for (auto& e : p->ev_lin) HIPCHK(hipEventCreate(&e));
+        for (auto& e : p->ev_step) HIPCHK(hipEventCreate(&e));
+    }
+    p->ev_used = 0;
+    p->timing = true;
+    return MCC_OK;
+}
+
+int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launches) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipStreamSynchronize(p->stream));
+    double lin = 0, st = 0;
+    const int n = p->ev_used / 2;
+    for (int i = 0; i < n; ++i) {
+        float a = 0, b = 0;
+        HIPCHK(hipEventElapsedTime(&a, p->ev_lin[2 * i], p->ev_lin[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&b, p->ev_step[2 * i], p->ev_step[2 * i + 1]));
+        lin += a;
+        st += b;
+    }
+    p->timing = false;
+    if (lin_ms) *lin_ms = n ? lin / n : 0.0;
+    if (step_ms) *step_ms = n ? st / n : 0.0;
+    if (launches) *launches = n;
+    return MCC_OK;
+}
+
+int mcc_problem_stats(const mcc_problem* p, long long* corners, long long* edges, long long* photos,
+                      long long* alg_bytes) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    if (corners) *corners = p->corners;
+    if (edges) *edges = p->E;
+    if (photos) *photos = p->V;
+    // 20 B per corner (float32 obj xyz + img uv) + 280 B per edge
+    if (alg_bytes) *alg_bytes = 20LL * p->corners + 280LL * p->E;
+    return MCC_OK;
+}
+
+// ---------------------------------------------------------------- multi-GPU
+int mcc_comm_unique_id(unsigned char* id) {
+    if (!id) return fail(MCC_EINVAL, "null id");
+    ncclUniqueId u;
+    ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    static_assert(sizeof(u.internal) == MCC_UNIQUE_ID_BYTES, "nccl id size");
+    std::memcpy(id, u.internal, MCC_UNIQUE_ID_BYTES);
+    return MCC_OK;
+}
+
+int mcc_comm_init(mcc_problem* p, const unsigned char* id, int nranks, int rank) {
+    if (!p || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(MCC_EINVAL, "bad comm arguments");
+    HIPCHK(hipSetDevice(p->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, MCC_UNIQUE_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&p->comm, nranks, u, rank);
+    if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    p->nranks = nranks;
+    p->rank = rank;
+    for (auto& g : p->gexec)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    return MCC_OK;
+}
+
+int mcc_comm_allreduce_max(mcc_problem* p, double* v) {
+    if (!p || !v) return fail(MCC_EINVAL, "null argument");
+    if (!p->comm || p->nranks == 1) return MCC_OK;
+    HIPCHK(hipSetDevice(p->device));
+    double* dv;
+    HIPCHK(hipMalloc((void**)&dv, sizeof(double)));
+    HIPCHK(hipMemcpy(dv, v, sizeof(double), hipMemcpyHostToDevice));
+    ncclResult_t r = ncclAllReduce(dv, dv, 1, ncclDouble, ncclMax, p->comm, p->stream);
+    if (r != ncclSuccess) { (void)hipFree(dv); return fail(MCC_ECOMM, ncclGetErrorString(r)); }
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(v, dv, sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipFree(dv));
+    return MCC_OK;
+}
+
+int mcc_comm_barrier(mcc_problem* p) {
+    double v = 0.0;
+    int rc = mcc_comm_allreduce_max(p, &v);
+    if (rc) return rc;
+    HIPCHK(hipDeviceSynchronize());
+    return MCC_OK;
+}
+
+int mcc_partition_photos(int n_photos, int n_edges, const int* edge_photo, const int* edge_n, int nranks,
+                         int* rank_of_photo) {
+    if (n_photos < 0 || nranks < 1 || !rank_of_photo || (n_edges && (!edge_photo || !edge_n)))
+        return fail(MCC_EINVAL, "bad partition arguments");
+    std::vector<long long> w(n_photos, 0);
+    for (int e = 0; e < n_edges; ++e) {
+        if (edge_photo[e] < 0 || edge_photo[e] >= n_photos) return fail(MCC_EINVAL, "edge_photo out of range");
+        w[edge_photo[e]] += edge_n[e];
+    }
+    std::vector<int> ord(n_photos);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return w[a] > w[b]; });
+    std::vector<long long> load(nranks, 0);
+    for (int v : ord) {
+        int best = 0;
+        for (int r = 1; r < nranks; ++r)
+            if (load[r] < load[best]) best = r;
+        rank_of_photo[v] = best;
+        load[best] += w[v];
+    }
+    return MCC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,107 @@
+// mcc_internal.h -- device state and kernel argument blocks shared by mcc_kernels.hip and
+// mcc_api.cpp.  Not part of the public ABI (include/mcc.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/mcc.h"
+
+namespace mcc {
+
+// Device-resident loop state of optimizeExtrinsics (src/multicalib.cpp:468-507).
+struct State {
+    int iter;         // completed updates k
+    int done;         // stop test fired
+    int crit_type;    // 0 = never stop (bench / linearize-only), 1 COUNT, 2 EPS, 3 COUNT+EPS
+    int max_count;
+    double eps;
+    double change;    // ||G|| / ||x|| of the last update
+    double alpha;     // 0.95^(k+1) of the running step
+    double cam_normG2, cam_normX2;   // global-block partials of the last update
+    int error;        // bit 0: photo block not PD, bit 1: camera system not PD
+    int pad;
+};
+
+struct LinArgs {
+    State* state;
+    const int* photo_ptr;     // [V+1] photo-major edge ranges
+    const int4* edge_info;    // [E] {cam, side, corner_off, n}
+    const float* obj_x; const float* obj_y; const float* obj_z;   // [corners] photo-major
+    const float* img_u; const float* img_v;
+    const float* x;           // [P] float32 parameters [global m | photos]
+    const float* K; const float* D; const float* xi;
+    const float* cam_rt;      // DOUBLESIDE fixed cameras (rvec, tvec) [6C]
+    const double* ds_rt;      // PINHOLE doubleSideTransform (rvec, tvec) [6]
+    int nd, global_dim;
+    // outputs
+    double* Y;        // [36E] Schur factors Hgp_e L_p^-T
+    double* Hgg;      // [36E]
+    double* gg;       // [6E]
+    double* Lp;       // [36V]
+    double* zp;       // [6V]
+    double* gp_tot;   // [6V] photo JTE
+    float* resid;     // optional [2*corners] float32 residuals (debug)
+};
+
+struct SchurArgs {
+    const State* state;
+    const int4* items;   // {block, pair_begin, pair_end, diag}
+    const int4* pairs;   // {e1, e2, photo, self}
+    const double* Y; const double* Hgg; const double* gg; const double* zp;
+    double* item_out;    // [42 * items]
+};
+
+struct AsmArgs {
+    State* state;
+    const int* block_items;   // [nblk + 1]
+    const double* item_out;
+    const int* gblock_ptr; const int* gblock_edges;
+    const double* gg;
+    const double* photo_norm;  // [2V]
+    double* packed;
+    int m, n_photos, rank;
+};
+
+struct SolveArgs {
+    State* state;
+    const double* packed;
+    const double* alpha; int n_alpha;
+    float* x;
+    double* dg;       // [m]
+    double* delta;    // [P]
+    int m, do_update;
+};
+
+struct BacksubArgs {
+    const State* state;
+    const int* photo_ptr;
+    const int* edge_gblock;
+    const double* Y; const double* Lp; const double* zp; const double* dg;
+    float* x;
+    double* delta;
+    double* photo_norm;
+    int n_photos, m, do_update;
+};
+
+struct ErrArgs {
+    const int4* edge_info;
+    const int* edge_photo;
+    const float* obj_x; const float* obj_y; const float* obj_z;
+    const float* img_u; const float* img_v;
+    const float* x;
+    const float* K; const float* D; const float* xi;
+    const float* cam_pose;   // DOUBLESIDE [16C]
+    float* edge_sum;         // [E] device order
+    int nd, m;
+};
+
+}  // namespace mcc
+
+// launch wrappers (mcc_kernels.hip)
+size_t mcc_lin_shmem(int max_edges_per_photo);
+hipError_t mcc_set_lin_attrs(int max_epp);
+hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
+hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int n_items, hipStream_t s);
+hipError_t mcc_launch_assemble(const mcc::AsmArgs& a, hipStream_t s);
+hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
+hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
+hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s);

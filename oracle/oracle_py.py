@@ -1,0 +1,189 @@
+"""ctypes binding of the CPU oracle (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, as the checker.  The product (multi_camera_calibration_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_i32p = ctypes.POINTER(ctypes.c_int)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+class _OraProblem(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int), ("n_cams", ctypes.c_int), ("n_photos", ctypes.c_int),
+                ("n_edges", ctypes.c_int), ("edge_cam", _i32p), ("edge_photo", _i32p),
+                ("edge_side", _i32p), ("edge_off", _i32p), ("edge_n", _i32p),
+                ("obj", _f32p), ("img", _f32p), ("nd", ctypes.c_int), ("K", _f32p),
+                ("D", _f32p), ("xi", _f32p), ("ds_pose", _f64p), ("cam_pose", _f32p)]
+
+
+def build(force: bool = False) -> str:
+    so = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "mcc_oracle.c")
+    if force or not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", _HERE, "-s", "liboracle.so"], check=True)
+    return so
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = ctypes.CDLL(build())
+        L = _LIB
+        L.ora_optimize.restype = ctypes.c_double
+        L.ora_num_threads.restype = ctypes.c_int
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+class Oracle:
+    """Holds contiguous copies of a rig.Problem and a ctypes ora_problem view of them."""
+
+    def __init__(self, prob):
+        self.prob = prob
+        self._keep = []
+
+        def arr(a, dt):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, dtype=dt)
+            self._keep.append(a)
+            return a
+        s = _OraProblem()
+        s.model, s.n_cams, s.n_photos = prob.model, prob.n_cams, prob.n_photos
+        s.n_edges = prob.n_edges
+        s.edge_cam = _p(arr(prob.edge_cam, np.int32), _i32p)
+        s.edge_photo = _p(arr(prob.edge_photo, np.int32), _i32p)
+        s.edge_side = _p(arr(prob.edge_side, np.int32), _i32p)
+        s.edge_off = _p(arr(prob.edge_off, np.int32), _i32p)
+        s.edge_n = _p(arr(prob.edge_n, np.int32), _i32p)
+        s.obj = _p(arr(prob.obj, np.float32), _f32p)
+        s.img = _p(arr(prob.img, np.float32), _f32p)
+        s.nd = prob.nd
+        s.K = _p(arr(prob.K, np.float32), _f32p)
+        s.D = _p(arr(prob.D, np.float32), _f32p)
+        s.xi = _p(arr(prob.xi, np.float32), _f32p)
+        s.ds_pose = _p(arr(prob.ds_pose, np.float64), _f64p)
+        s.cam_pose = _p(arr(prob.cam_pose, np.float32), _f32p)
+        self.s = s
+        self.P = lib().ora_nparams(ctypes.byref(s))
+
+    def edge_linearize(self, x, e):
+        n = int(self.prob.edge_n[e])
+        x = np.ascontiguousarray(x, np.float32)
+        jc = np.zeros((2 * n, 6)); jp = np.zeros((2 * n, 6)); E = np.zeros(2 * n)
+        proj = np.zeros(2 * n, np.float32)
+        rc = lib().ora_edge_linearize(ctypes.byref(self.s), _p(x, _f32p), e, _p(jc, _f64p),
+                                      _p(jp, _f64p), _p(E, _f64p), _p(proj, _f32p))
+        if rc:
+            raise RuntimeError(f"ora_edge_linearize failed: {rc}")
+        return jc, jp, E, proj
+
+    def normal_dense(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        JTJ = np.zeros((self.P, self.P)); JTE = np.zeros(self.P)
+        rc = lib().ora_normal_dense(ctypes.byref(self.s), _p(x, _f32p), _p(JTJ, _f64p), _p(JTE, _f64p))
+        if rc:
+            raise RuntimeError(f"ora_normal_dense failed: {rc}")
+        return JTJ, JTE
+
+    def linearize_solve(self, x, solver="schur"):
+        x = np.ascontiguousarray(x, np.float32)
+        d = np.zeros(self.P); jte = np.zeros(self.P)
+        rc = lib().ora_linearize_solve(ctypes.byref(self.s), _p(x, _f32p), 1 if solver == "schur" else 0,
+                                       _p(d, _f64p), _p(jte, _f64p))
+        if rc:
+            raise RuntimeError(f"ora_linearize_solve failed: {rc}")
+        return d, jte
+
+    def schur_partial(self, x, lo, hi):
+        x = np.ascontiguousarray(x, np.float32)
+        m = lib().ora_global_dim(ctypes.byref(self.s))
+        S = np.zeros((m, m)); r = np.zeros(m)
+        rc = lib().ora_schur_partial(ctypes.byref(self.s), _p(x, _f32p), lo, hi, _p(S, _f64p), _p(r, _f64p))
+        if rc:
+            raise RuntimeError(f"ora_schur_partial failed: {rc}")
+        return S, r
+
+    def optimize(self, x, crit_type=3, max_count=200, eps=1e-7, solver="schur"):
+        x = np.array(x, np.float32, copy=True)
+        it = ctypes.c_int(0); ch = ctypes.c_double(0)
+        mean = lib().ora_optimize(ctypes.byref(self.s), crit_type, max_count, ctypes.c_double(eps),
+                                  1 if solver == "schur" else 0, _p(x, _f32p), ctypes.byref(it),
+                                  ctypes.byref(ch))
+        if mean < 0:
+            raise RuntimeError("ora_optimize failed")
+        return x, mean, it.value, ch.value
+
+    def project_error(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        err = np.zeros(self.prob.n_edges, np.float32)
+        mean = ctypes.c_double(0)
+        rc = lib().ora_project_error(ctypes.byref(self.s), _p(x, _f32p), _p(err, _f32p), ctypes.byref(mean))
+        if rc:
+            raise RuntimeError(f"ora_project_error failed: {rc}")
+        return err, mean.value
+
+
+def rodrigues_v2m(r):
+    r = np.ascontiguousarray(r, np.float64)
+    R = np.zeros(9); J = np.zeros(27)
+    lib().ora_rodrigues_v2m(_p(r, _f64p), _p(R, _f64p), _p(J, _f64p))
+    return R.reshape(3, 3), J.reshape(3, 9)
+
+
+def rodrigues_m2v(R):
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    r = np.zeros(3); J = np.zeros(27)
+    lib().ora_rodrigues_m2v(_p(R, _f64p), _p(r, _f64p), _p(J, _f64p))
+    return r, J.reshape(9, 3)
+
+
+def compose_motion(om1, T1, om2, T2):
+    a = [np.ascontiguousarray(v, np.float64) for v in (om1, T1, om2, T2)]
+    om3 = np.zeros(3); T3 = np.zeros(3); d = np.zeros((8, 9))
+    lib().ora_compose_motion(*[_p(v, _f64p) for v in a], _p(om3, _f64p), _p(T3, _f64p), _p(d, _f64p))
+    return om3, T3, d.reshape(8, 3, 3)
+
+
+def project_pinhole(obj, rvec, tvec, K, D, jac=True):
+    obj = np.ascontiguousarray(obj, np.float32)
+    n = obj.shape[0]
+    rv = np.ascontiguousarray(rvec, np.float32); tv = np.ascontiguousarray(tvec, np.float32)
+    K = np.ascontiguousarray(K, np.float32); D = np.ascontiguousarray(D, np.float32)
+    img = np.zeros(2 * n, np.float32)
+    J = np.zeros((2 * n, 6)) if jac else None
+    rc = lib().ora_project_pinhole(n, _p(obj, _f32p), _p(rv, _f32p), _p(tv, _f32p), _p(K, _f32p),
+                                   _p(D, _f32p), int(D.size), _p(img, _f32p), _p(J, _f64p))
+    if rc:
+        raise RuntimeError("ora_project_pinhole failed")
+    return img.reshape(n, 2), J
+
+
+def project_omni(obj, rvec, tvec, K, xi, D, jac=True):
+    obj = np.ascontiguousarray(obj, np.float32)
+    n = obj.shape[0]
+    rv = np.ascontiguousarray(rvec, np.float32); tv = np.ascontiguousarray(tvec, np.float32)
+    K = np.ascontiguousarray(K, np.float32); D = np.ascontiguousarray(D, np.float32)
+    img = np.zeros(2 * n, np.float32)
+    J = np.zeros((2 * n, 6)) if jac else None
+    lib().ora_project_omni(n, _p(obj, _f32p), _p(rv, _f32p), _p(tv, _f32p), _p(K, _f32p),
+                           ctypes.c_double(float(np.float32(xi))), _p(D, _f32p), _p(img, _f32p), _p(J, _f64p))
+    return img.reshape(n, 2), J
+
+
+def num_threads():
+    return lib().ora_num_threads()
