@@ -129,6 +129,9 @@ int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
  * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
+/* diagnostic build only (libmcc_diag.so, -DMCC_DIAG): first call arms per-phase s_memtime
+ * stamps of k_linearize, later calls copy [16 * n_photos] stamps out (others: MCC_EINVAL) */
+int mcc_debug_stamps(mcc_problem *p, long long *out, int n);
 /* static facts about the problem for roofline accounting */
 int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges,
                       long long *photos, long long *alg_bytes_per_step);

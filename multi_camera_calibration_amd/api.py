@@ -22,7 +22,7 @@ import numpy as np
 from . import rig as _rig
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmcc.so")
+LIB_PATH = os.environ.get("MCC_LIB") or os.path.join(_HERE, "libmcc.so")   # MCC_LIB: libmcc_diag.so for stamps
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "mcc.h")
 
 _i32p = ctypes.POINTER(ctypes.c_int)
@@ -87,6 +87,7 @@ def lib():
         L.mcc_comm_allreduce_max.argtypes = [ctypes.c_void_p, _f64p]
         L.mcc_comm_barrier.argtypes = [ctypes.c_void_p]
         L.mcc_partition_photos.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p]
+        L.mcc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -232,6 +233,13 @@ class BundleAdjuster:
         v = [ctypes.c_longlong(0) for _ in range(4)]
         _check(lib().mcc_problem_stats(self.h, *[ctypes.byref(t) for t in v]), "mcc_problem_stats")
         return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
+
+    def stamps(self):
+        """libmcc_diag.so only: first call arms, later calls return [n_photos, 16] s_memtime stamps."""
+        out = np.zeros(16 * max(self.prob.n_photos, 1), np.int64)
+        _check(lib().mcc_debug_stamps(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), out.size),
+               "mcc_debug_stamps")
+        return out.reshape(-1, 16)
 
     # -- multi-GPU
     def comm_init(self, uid: bytes, nranks: int, rank: int):

@@ -107,7 +107,7 @@ struct mcc_problem {
     int model = 0, C = 0, V = 0, E = 0, nd = 0, m = 0, P = 0, device = 0;
     long long corners = 0;
     bool rational = false, prism = false;
-    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0;
+    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
     hipStream_t stream = nullptr;
 
     // host-side maps
@@ -117,8 +117,9 @@ struct mcc_problem {
 
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
+    DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha;
-    DevBuf<int> photo_ptr, edge_gblock, block_items, gblock_ptr, gblock_edges, edge_photo;
+    DevBuf<int> photo_ptr, edge_gblock, block_items, edge_photo, counter;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
@@ -141,6 +142,10 @@ struct mcc_problem {
 
 namespace {
 
+mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
+    return mcc::SolveCtx{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+}
+
 int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     using namespace mcc;
     const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
@@ -159,28 +164,47 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.gg = p->gg.p; la.Lp = p->Lp.p; la.zp = p->zp.p;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
+    la.gblock = p->edge_gblock.p;
+    la.dg = p->dg.p;
+    la.photo_norm = p->photo_norm.p;
+    la.stamps = p->stamps.p;
     if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
 
-    SchurArgs sa{p->state.p, p->items.p, p->pairs.p, p->Y.p, p->Hgg.p, p->gg.p, p->zp.p, p->item_out.p};
-    HIPCHK(mcc_launch_schur(sa, p->n_items, p->stream));
-    AsmArgs aa{p->state.p, p->block_items.p, p->item_out.p, p->gblock_ptr.p, p->gblock_edges.p, p->gg.p,
-               p->photo_norm.p, p->packed.p, p->m, p->V, p->rank};
-    HIPCHK(mcc_launch_assemble(aa, p->stream));
-    if (p->comm && p->nranks > 1) {
+    const bool multi = p->comm && p->nranks > 1;
+    SchurArgs sa{};
+    sa.state = p->state.p;
+    sa.items = p->items.p; sa.pairs = p->pairs.p;
+    sa.Y = p->Y.p; sa.Hgg = p->Hgg.p; sa.gg = p->gg.p; sa.zp = p->zp.p;
+    sa.item_out = p->item_out.p;
+    sa.n_items = p->n_items;
+    sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
+    sa.counter = p->counter.p;
+    sa.block_items = p->block_items.p;
+    sa.packed = p->packed.p;
+    sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = multi ? 0 : 1;
+    sa.solve = solve_ctx(p, do_update);
+    HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
+    if (multi) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                        p->comm, p->stream);
         if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        SolveArgs so{solve_ctx(p, do_update), p->packed.p};
+        HIPCHK(mcc_launch_solve(so, p->stream));
     }
-    SolveArgs so{p->state.p, p->packed.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
-    HIPCHK(mcc_launch_solve(so, p->stream));
-    BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->Lp.p, p->zp.p, p->dg.p,
-                   p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
-    HIPCHK(mcc_launch_backsub(ba, p->stream));
     if (tim) {
         HIPCHK(hipEventRecord(p->ev_step[p->ev_used + 1], p->stream));
         p->ev_used += 2;
     }
+    return MCC_OK;
+}
+
+// standalone photo back-substitution: deltaX of the photos (do_update = 0) or a flush of the
+// pending update (do_update = 1)
+int enqueue_backsub(mcc_problem* p, int do_update) {
+    mcc::BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->Lp.p, p->zp.p, p->dg.p,
+                        p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
+    HIPCHK(mcc_launch_backsub(ba, p->stream));
     return MCC_OK;
 }
 
@@ -219,6 +243,8 @@ int launch_update_steps(mcc_problem* p, int n) {
     return MCC_OK;
 }
 
+int read_state(mcc_problem* p);
+
 int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, double eps) {
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
@@ -233,6 +259,17 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     p->h_state->eps = eps;
     p->h_state->error = 0;
     HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
+    return MCC_OK;
+}
+
+int flush_pending(mcc_problem* p) {
+    int rc = read_state(p);
+    if (rc) return rc;
+    if (!p->h_state->pending) return MCC_OK;
+    if ((rc = enqueue_backsub(p, 1))) return rc;
+    HIPCHK(hipStreamSynchronize(p->stream));
+    p->h_state->pending = 0;
+    HIPCHK(hipMemcpy(&p->state.p->pending, &p->h_state->pending, sizeof(int), hipMemcpyHostToDevice));
     return MCC_OK;
 }
 
@@ -359,12 +396,14 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         }
     std::vector<int4> pairs, items;
     std::vector<int> block_items(p->nblk + 1, 0);
-    const int kItemPairs = 192;
     for (int b = 0; b < p->nblk; ++b) {
         const int begin = (int)pairs.size();
         pairs.insert(pairs.end(), blk_pairs[b].begin(), blk_pairs[b].end());
         const int end = (int)pairs.size();
-        for (int s = begin; s < end; s += kItemPairs) items.push_back(make_int4(b, s, std::min(end, s + kItemPairs), 0));
+        // <= 24 work items per block keeps the last-arriver assembly short; >= 20 pairs per item
+        // (4 per sub-chunk thread) keeps the item workgroups busy
+        const int per_item = std::max(20, (end - begin + 23) / 24);
+        for (int s = begin; s < end; s += per_item) items.push_back(make_int4(b, s, std::min(end, s + per_item), 0));
         block_items[b + 1] = (int)items.size();
     }
     for (int b1 = 0; b1 < nb; ++b1)
@@ -372,12 +411,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             return bail(fail(MCC_EINVAL, "global block " + std::to_string(b1) + " has no observations"));
     p->n_items = (int)items.size();
     p->n_pairs = (int)pairs.size();
-    std::vector<int> gptr(nb + 1, 0), gedges;
-    for (int b = 0; b < nb; ++b) {
-        for (int e = 0; e < E; ++e)
-            if (gblock[e] == b) gedges.push_back(e);
-        gptr[b + 1] = (int)gedges.size();
-    }
+    p->n_norm_chunks = (V + 255) / 256;
+    if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
 
     // ---- fixed transforms
     std::vector<float> cam_rt(6 * C, 0.f);
@@ -423,12 +458,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->pairs.upload(pairs.data(), pairs.size()));
     HIPC(p->items.upload(items.data(), items.size()));
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
-    HIPC(p->gblock_ptr.upload(gptr.data(), gptr.size()));
-    HIPC(p->gblock_edges.upload(gedges.data(), gedges.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E)); HIPC(p->Hgg.alloc(36 * (size_t)E)); HIPC(p->gg.alloc(6 * (size_t)E));
     HIPC(p->Lp.alloc(36 * (size_t)V)); HIPC(p->zp.alloc(6 * (size_t)V)); HIPC(p->gp_tot.alloc(6 * (size_t)V));
-    HIPC(p->item_out.alloc(42 * (size_t)items.size()));
+    HIPC(p->item_out.alloc(48 * (size_t)(items.size() + p->n_norm_chunks)));
+    HIPC(p->counter.alloc(1));
+    HIPC(hipMemset(p->counter.p, 0, sizeof(int)));
     p->ntri = p->m * (p->m + 1) / 2;
     p->packed_len = p->ntri + 2 * p->m + 2;
     HIPC(p->packed.alloc(p->packed_len));
@@ -441,7 +476,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     std::memset(p->h_state, 0, sizeof(State));
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
-    HIPC(mcc_set_lin_attrs(p->max_epp));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, p->m));
     if (mcc_lin_shmem(p->max_epp) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
 #undef HIPC
     (void)rc;
@@ -460,12 +495,12 @@ void mcc_destroy(mcc_problem* p) {
     if (p->comm) (void)ncclCommDestroy(p->comm);
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
-    p->cam_pose.release(); p->resid.release(); p->edge_sum.release();
+    p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Lp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
-    p->photo_ptr.release(); p->edge_gblock.release(); p->block_items.release(); p->gblock_ptr.release();
-    p->gblock_edges.release(); p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
+    p->photo_ptr.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release();
+    p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -477,12 +512,16 @@ int mcc_set_params(mcc_problem* p, const float* x, int n) {
     HIPCHK(hipSetDevice(p->device));
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->x.p, x, sizeof(float) * n, hipMemcpyHostToDevice));
+    const int zero = 0;   // the new x supersedes any pending photo update
+    HIPCHK(hipMemcpy(&p->state.p->pending, &zero, sizeof(int), hipMemcpyHostToDevice));
     return MCC_OK;
 }
 
 int mcc_get_params(mcc_problem* p, float* x, int n) {
     if (!p || !x || n != p->P) return fail(MCC_EINVAL, "mcc_get_params: size mismatch");
     HIPCHK(hipSetDevice(p->device));
+    int rc = flush_pending(p);
+    if (rc) return rc;
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(x, p->x.p, sizeof(float) * n, hipMemcpyDeviceToHost));
     return MCC_OK;
@@ -491,10 +530,11 @@ int mcc_get_params(mcc_problem* p, float* x, int n) {
 int mcc_linearize_solve(mcc_problem* p, double* delta, double* jte) {
     if (!p) return fail(MCC_EINVAL, "null problem");
     HIPCHK(hipSetDevice(p->device));
-    int rc = set_state(p, 0, 0, 0, 0.0);
+    int rc = flush_pending(p);
     if (rc) return rc;
-    rc = enqueue_step(p, 0, nullptr);
-    if (rc) return rc;
+    if ((rc = set_state(p, 0, 0, 0, 0.0))) return rc;
+    if ((rc = enqueue_step(p, 0, nullptr))) return rc;
+    if ((rc = enqueue_backsub(p, 0))) return rc;
     if ((rc = read_state(p))) return rc;
     if ((rc = check_state_error(p))) return rc;
     if (delta) HIPCHK(hipMemcpy(delta, p->delta.p, sizeof(double) * p->P, hipMemcpyDeviceToHost));
@@ -590,6 +630,25 @@ int mcc_debug_residuals(mcc_problem* p, const float* x, float* res) {
         res[2 * p->dev2ref_corner[c] + 1] = r[2 * c + 1];
     }
     return MCC_OK;
+}
+
+int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
+#ifdef MCC_DIAG
+    if (!p || !out) return fail(MCC_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    if (!p->stamps.p) {
+        HIPCHK(p->stamps.alloc(16 * (size_t)std::max(p->V, 1)));
+        HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * 16 * std::max(p->V, 1)));
+        return MCC_OK;   // armed: the next linearisations record
+    }
+    HIPCHK(hipStreamSynchronize(p->stream));
+    const int cnt = std::min(n, 16 * p->V);
+    HIPCHK(hipMemcpy(out, p->stamps.p, sizeof(long long) * cnt, hipMemcpyDeviceToHost));
+    return MCC_OK;
+#else
+    (void)p; (void)out; (void)n;
+    return fail(MCC_EINVAL, "mcc_debug_stamps needs the MCC_DIAG build (libmcc_diag.so)");
+#endif
 }
 
 int mcc_timing_begin(mcc_problem* p) {

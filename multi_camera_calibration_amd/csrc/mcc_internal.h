@@ -18,7 +18,7 @@ struct State {
     double alpha;     // 0.95^(k+1) of the running step
     double cam_normG2, cam_normX2;   // global-block partials of the last update
     int error;        // bit 0: photo block not PD, bit 1: camera system not PD
-    int pad;
+    int pending;      // a solved photo update waits to be applied by the next k_linearize
 };
 
 struct LinArgs {
@@ -27,7 +27,7 @@ struct LinArgs {
     const int4* edge_info;    // [E] {cam, side, corner_off, n}
     const float* obj_x; const float* obj_y; const float* obj_z;   // [corners] photo-major
     const float* img_u; const float* img_v;
-    const float* x;           // [P] float32 parameters [global m | photos]
+    float* x;                 // [P] float32 parameters [global m | photos] (photo part updated in place)
     const float* K; const float* D; const float* xi;
     const float* cam_rt;      // DOUBLESIDE fixed cameras (rvec, tvec) [6C]
     const double* ds_rt;      // PINHOLE doubleSideTransform (rvec, tvec) [6]
@@ -40,30 +40,15 @@ struct LinArgs {
     double* zp;       // [6V]
     double* gp_tot;   // [6V] photo JTE
     float* resid;     // optional [2*corners] float32 residuals (debug)
+    // pending update of the previous step (fused back-substitution)
+    const int* gblock;       // [E] global block of an edge or -1
+    const double* dg;        // [m] global-block delta of the previous solve
+    double* photo_norm;      // [2V] ||G||^2, ||x||^2 partials of the applied update
+    long long* stamps;       // MCC_DIAG builds: [16V] s_memtime per phase
 };
 
-struct SchurArgs {
-    const State* state;
-    const int4* items;   // {block, pair_begin, pair_end, diag}
-    const int4* pairs;   // {e1, e2, photo, self}
-    const double* Y; const double* Hgg; const double* gg; const double* zp;
-    double* item_out;    // [42 * items]
-};
-
-struct AsmArgs {
+struct SolveCtx {
     State* state;
-    const int* block_items;   // [nblk + 1]
-    const double* item_out;
-    const int* gblock_ptr; const int* gblock_edges;
-    const double* gg;
-    const double* photo_norm;  // [2V]
-    double* packed;
-    int m, n_photos, rank;
-};
-
-struct SolveArgs {
-    State* state;
-    const double* packed;
     const double* alpha; int n_alpha;
     float* x;
     double* dg;       // [m]
@@ -71,10 +56,30 @@ struct SolveArgs {
     int m, do_update;
 };
 
+struct SchurArgs {
+    State* state;
+    const int4* items;   // {block, pair_begin, pair_end, -}
+    const int4* pairs;   // {e1, e2, photo, self}
+    const double* Y; const double* Hgg; const double* gg; const double* zp;
+    double* item_out;    // [48 * (items + norm chunks)]
+    int n_items;
+    const double* photo_norm; int n_photos;
+    int* counter;        // ticket for the last-arriving workgroup (zero between launches)
+    const int* block_items;   // [nblk + 1]
+    double* packed;
+    int m, rank, fuse_solve;
+    SolveCtx solve;
+};
+
+struct SolveArgs {
+    SolveCtx ctx;
+    const double* packed;
+};
+
 struct BacksubArgs {
     const State* state;
     const int* photo_ptr;
-    const int* edge_gblock;
+    const int* gblock;
     const double* Y; const double* Lp; const double* zp; const double* dg;
     float* x;
     double* delta;
@@ -98,10 +103,10 @@ struct ErrArgs {
 
 // launch wrappers (mcc_kernels.hip)
 size_t mcc_lin_shmem(int max_edges_per_photo);
-hipError_t mcc_set_lin_attrs(int max_epp);
+size_t mcc_solve_shmem(int m);
+hipError_t mcc_set_kernel_attrs(int max_epp, int m);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
-hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int n_items, hipStream_t s);
-hipError_t mcc_launch_assemble(const mcc::AsmArgs& a, hipStream_t s);
+hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
 hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s);

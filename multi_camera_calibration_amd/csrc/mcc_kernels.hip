@@ -1,17 +1,18 @@
 // mcc_kernels.hip -- CDNA4 (gfx950) kernels of one Gauss-Newton step of the reference's
 // multi-camera extrinsic BA (MultiCameraCalibration::optimizeExtrinsics, src/multicalib.cpp:462-514).
 //
-// Step dataflow:
+// Step dataflow, single GPU = 2 launches:
 //   k_linearize   one workgroup per photo vertex, one wavefront per edge (camera observing it):
-//                 edge prologue (compose_motion + fl32 pose, one lane per edge), corner sweep
-//                 (lanes over corners, FP64 projection + 2x6 Jacobian strips, float32 residual),
-//                 butterfly reduce-scatter of the 27 normal-equation sums, chain rule to the
-//                 photo / global blocks, 6x6 photo Cholesky and the Schur factors Y_e = H_gp L^-T.
-//   k_schur       camera-pair blocks of S = sum H_gg - sum Y_e Y_e'^T and r, per work item.
-//   k_assemble    deterministic sum of the work items + norm partials into the packed buffer
-//                 that multi-GPU runs all-reduce over RCCL.
-//   k_solve       stop test (src/multicalib.cpp:475-477), Cholesky of S, global-block update.
-//   k_backsub     photo back-substitution and float32 update x = fl32(x + fl32(a*delta)).
+//                 [pending photo update of the previous step: back-substitution + float32
+//                 update, fused here], edge prologue (compose_motion + fl32 pose, one lane per
+//                 edge), corner sweep (lanes over corners, FP64 projection + 2x6 Jacobian strips,
+//                 float32 residual), butterfly reduce-scatter of the 27 normal-equation sums,
+//                 chain rule to the photo / global blocks, 6x6 photo Cholesky, Y_e = H_gp L^-T.
+//   k_schur       work items of camera-pair blocks of S = sum H_gg - sum Y_e Y_e'^T and r, plus
+//                 norm chunks; the last-arriving workgroup assembles the packed system in fixed
+//                 order and (single GPU) solves it: stop test, Cholesky, global-block update.
+//   multi-GPU:    k_schur assembles only -> RCCL all-reduce of the packed system -> k_solve.
+//   k_backsub     standalone photo back-substitution (flush of a pending update / deltaX output).
 // No MFMA: the largest dense block is 6x6; the path is FP64-VALU and
 // latency bound.  All reductions are fixed-order, so a run is bitwise reproducible.
 #include <hip/hip_runtime.h>
@@ -22,16 +23,16 @@
 namespace mcc {
 
 // ---------------------------------------------------------------- wave reduction
-// Reduce-scatter butterfly of NV (<= 32) per-lane doubles across the 64 lanes: 32 shuffles of
-// 64-bit values instead of 6*NV.  Afterwards lane l (and l^1) holds the full sum of value
-// index idx(l) = 16*b5 + 8*b4 + 4*b3 + 2*b2 + b1.
+// Reduce-scatter butterfly of 32 per-lane doubles across the 64 lanes: 32 shuffles of 64-bit
+// values instead of 6*27.  Afterwards lane l (and l^1) holds the full sum of value index
+// idx(l) = 16*b5 + 8*b4 + 4*b3 + 2*b2 + b1.
 template <int W>
 __device__ __forceinline__ void bfly_step(double* v, int lane) {
     const bool hi = (lane & (2 * W)) != 0;
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-        double send = hi ? v[j] : v[j + W];
-        double keep = hi ? v[j + W] : v[j];
+        const double send = hi ? v[j] : v[j + W];
+        const double keep = hi ? v[j + W] : v[j];
         v[j] = keep + __shfl_xor(send, 2 * W);
     }
 }
@@ -46,6 +47,12 @@ __device__ __forceinline__ double wave_reduce_scatter32(double* v, int lane) {
 __device__ __forceinline__ int bfly_index(int lane) {
     return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
            ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
+}
+// fixed-order full wave sum (xor butterfly)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
 // ---------------------------------------------------------------- per-edge LDS record
@@ -65,103 +72,124 @@ struct EdgeLds {
     int has_global, edge, pad0, pad1;
 };
 static_assert(sizeof(EdgeLds) % 16 == 0, "EdgeLds alignment");
+constexpr int kPhotoScratch = 96;   // doubles after the edge records
+
+// G (6x6) = [[Grr, 0], [Gtr, Gtt]]; Gtt == nullptr means identity.
+__device__ __forceinline__ void store_G(double* G, const double* Grr, const double* Gtr, const double* Gtt) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            G[i * 6 + j] = Grr ? Grr[i * 3 + j] : 0.0;
+            G[i * 6 + 3 + j] = 0.0;
+            G[(3 + i) * 6 + j] = Gtr ? Gtr[i * 3 + j] : 0.0;
+            G[(3 + i) * 6 + 3 + j] = Gtt ? Gtt[i * 3 + j] : (i == j ? 1.0 : 0.0);
+        }
+}
 
 // ---------------------------------------------------------------- edge prologue (one lane)
+// compose_motion(photo, camera) [+ compose_motion(ds, photofront) for BACK edges], float32
+// composed pose, Rodrigues of it for the projection, and the chain maps G = blockdiag(Jl, I) M.
+// src/mymulticalib.cpp:468-614 (pinhole), src/multicalib.cpp:717-824 (omni),
+// src/doubleSide.cpp:288-430 (double side).
 template <int MODEL>
-__device__ void edge_prologue(const LinArgs& a, int photo, int e, EdgeLds& L) {
+__device__ void edge_prologue(const LinArgs& a, const double* xp, int e, EdgeLds& L) {
     const int4 info = a.edge_info[e];
     const int cam = info.x, side = info.y;
-    const float* x = a.x;
-    const int pc = a.global_dim + 6 * photo;
-    double om1[3], T1[3], om2[3], T2[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { om1[k] = x[pc + k]; T1[k] = x[pc + 3 + k]; }
+    double om1[3] = {xp[0], xp[1], xp[2]}, T1[3] = {xp[3], xp[4], xp[5]};
+    double om2[3], T2[3];
     if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * cam + k]; T2[k] = a.cam_rt[6 * cam + 3 + k]; }
     } else if (cam == 0) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }
+        for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
     } else {
-        const int cc = 6 * (cam - 1);
+        const float* xc = a.x + 6 * (cam - 1);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { om2[k] = x[cc + k]; T2[k] = x[cc + 3 + k]; }
+        for (int k = 0; k < 3; ++k) { om2[k] = xc[k]; T2[k] = xc[3 + k]; }
     }
+    Rot r1, r2;
+    rodrigues_v2m(om1, r1);
+    rodrigues_v2m(om2, r2);
+    double Jr1[9], Jl2[9];
+    so3_jac(om1, r1, -1.0, Jr1);
+    so3_jac(om2, r2, +1.0, Jl2);
     Motion f;
-    compose_motion(om1, T1, om2, T2, f);
-    double Mp[36], Mg[36];
-#pragma unroll
-    for (int k = 0; k < 36; ++k) { Mp[k] = 0.0; Mg[k] = 0.0; }
+    compose(r1.R, Jr1, T1, r2.R, Jl2, T2, f);
     double om[3], T[3];
+    double GpRR[9], GpTR[9], GgRR[9], GgTR[9];   // pre-Jl blocks (rows 0-2 get Jl applied below)
+    const double* GgTT = nullptr;                // nullptr: identity
+    double Rf[9];
     int has_global;
+    bool gg_zero = false, gg_tr_zero = false, gp_tr_zero = true;
     if (side == MCC_BACK) {
         double dsr[3], dst[3];
         if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k) { dsr[k] = x[k]; dst[k] = x[3 + k]; }
+            for (int k = 0; k < 3; ++k) { dsr[k] = a.x[k]; dst[k] = a.x[3 + k]; }
         } else {
 #pragma unroll
             for (int k = 0; k < 3; ++k) { dsr[k] = a.ds_rt[k]; dst[k] = a.ds_rt[3 + k]; }
         }
-        Motion b;   // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506
-        compose_motion(dsr, dst, f.om, f.T, b);
+        // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506: om2' = front om (FP64)
+        Rot rds, rfr;
+        rodrigues_v2m(dsr, rds);
+        rodrigues_v2m(f.om, rfr);
+        double Jrds[9], Jlf[9];
+        so3_jac(dsr, rds, -1.0, Jrds);
+        so3_jac(f.om, rfr, +1.0, Jlf);
+        Motion b;
+        compose(rds.R, Jrds, dst, rfr.R, Jlf, f.T, b);
 #pragma unroll
         for (int k = 0; k < 3; ++k) { om[k] = b.om[k]; T[k] = b.T[k]; }
-        // photo: E2 * D1 = [[A2b A1, 0], [B2b A1, R2]]
-        double t[9];
-        mat3_mul(b.A2, f.A1, t);
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) Mp[i * 6 + j] = t[i * 3 + j];
-        mat3_mul(b.B2, f.A1, t);
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) { Mp[(3 + i) * 6 + j] = t[i * 3 + j]; Mp[(3 + i) * 6 + 3 + j] = f.R2[i * 3 + j]; }
+        // photo: E2 * D1 = [[A2b A1, 0], [B2b A1, R2]]   (src/mymulticalib.cpp:509-512)
+        mat3_mul(b.A2, f.A1, GpRR);
+        mat3_mul(b.B2, f.A1, GpTR);
+        gp_tr_zero = false;
         if (MODEL == MCC_MODEL_DOUBLESIDE) {
             // ds block: [[A1b, 0], [0, R_front]]  (src/doubleSide.cpp:398-399)
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) { Mg[i * 6 + j] = b.A1[i * 3 + j]; Mg[(3 + i) * 6 + 3 + j] = f.R[i * 3 + j]; }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { GgRR[k] = b.A1[k]; Rf[k] = rfr.R[k]; }
+            GgTT = Rf;
+            gg_tr_zero = true;
             has_global = 1;
         } else {
             // camera block as the reference chains it (src/mymulticalib.cpp:514-517), which
             // omits dTt/dTf * dTf/dRc at :516 (hazard A12): [[A2b A2, 0], [B2b A2, I]]
-            mat3_mul(b.A2, f.A2, t);
-            for (int i = 0; i < 3; ++i)
-                for (int j = 0; j < 3; ++j) Mg[i * 6 + j] = t[i * 3 + j];
-            mat3_mul(b.B2, f.A2, t);
-            for (int i = 0; i < 3; ++i) {
-                for (int j = 0; j < 3; ++j) Mg[(3 + i) * 6 + j] = t[i * 3 + j];
-                Mg[(3 + i) * 6 + 3 + i] = 1.0;
-            }
+            mat3_mul(b.A2, f.A2, GgRR);
+            mat3_mul(b.B2, f.A2, GgTR);
             has_global = cam != 0;
         }
     } else {
 #pragma unroll
         for (int k = 0; k < 3; ++k) { om[k] = f.om[k]; T[k] = f.T[k]; }
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) { Mp[i * 6 + j] = f.A1[i * 3 + j]; Mp[(3 + i) * 6 + 3 + j] = f.R2[i * 3 + j]; }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) GpRR[k] = f.A1[k];
         if (MODEL == MCC_MODEL_DOUBLESIDE) {
-            has_global = 0;   // zero double-side jacobian on the front side (doubleSide.cpp:335-336)
+            gg_zero = true;   // zero double-side jacobian on the front side (doubleSide.cpp:335-336)
+            has_global = 0;
         } else {
-            for (int i = 0; i < 3; ++i) {
-                for (int j = 0; j < 3; ++j) { Mg[i * 6 + j] = f.A2[i * 3 + j]; Mg[(3 + i) * 6 + j] = f.B2[i * 3 + j]; }
-                Mg[(3 + i) * 6 + 3 + i] = 1.0;
-            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { GgRR[k] = f.A2[k]; GgTR[k] = f.B2[k]; }
             has_global = cam != 0;
         }
     }
     // Rvectran1 / Tvectran1 -> float32 (src/mymulticalib.cpp:546-553)
-    double rf[3], Jl[9];
+    double rf[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)om[k]; L.T[k] = (double)(float)T[k]; }
-    rodrigues_v2m(rf, L.R);
-    so3_jl(rf, Jl);
-    // G = blockdiag(Jl, I) * M
-    for (int j = 0; j < 6; ++j) {
-        for (int i = 0; i < 3; ++i) {
-            L.Gp[i * 6 + j] = Jl[i * 3] * Mp[j] + Jl[i * 3 + 1] * Mp[6 + j] + Jl[i * 3 + 2] * Mp[12 + j];
-            L.Gg[i * 6 + j] = Jl[i * 3] * Mg[j] + Jl[i * 3 + 1] * Mg[6 + j] + Jl[i * 3 + 2] * Mg[12 + j];
-            L.Gp[(3 + i) * 6 + j] = Mp[(3 + i) * 6 + j];
-            L.Gg[(3 + i) * 6 + j] = Mg[(3 + i) * 6 + j];
-        }
+    Rot rp;
+    rodrigues_v2m(rf, rp);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) L.R[k] = rp.R[k];
+    double Jl[9], t9[9];
+    so3_jac(rf, rp, +1.0, Jl);
+    mat3_mul(Jl, GpRR, t9);
+    store_G(L.Gp, t9, gp_tr_zero ? nullptr : GpTR, r2.R);
+    if (gg_zero) {
+        for (int k = 0; k < 36; ++k) L.Gg[k] = 0.0;
+    } else {
+        mat3_mul(Jl, GgRR, t9);
+        store_G(L.Gg, t9, gg_tr_zero ? nullptr : GgTR, GgTT);
     }
     L.cam = cam;
     L.side = side;
@@ -172,7 +200,7 @@ __device__ void edge_prologue(const LinArgs& a, int photo, int e, EdgeLds& L) {
 }
 
 // ---------------------------------------------------------------- per-corner models
-// Pinhole (cvProjectPoints2Internal order).  Returns float32 pixel and D = d(u,v)/dXc (2x3).
+// Pinhole (cvProjectPoints2Internal order).  Float32 pixel and D = d(u,v)/dXc (2x3).
 template <bool RATIONAL, bool PRISM>
 __device__ __forceinline__ void pinhole_corner(const double* R, const double* T, const double* k,
                                                double fx, double fy, double cx, double cy,
@@ -193,7 +221,7 @@ __device__ __forceinline__ void pinhole_corner(const double* R, const double* T,
         r2 = x * x + y * y;
         r4 = r2 * r2;
         r6 = r4 * r2;
-        double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
+        const double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
         cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
         icdist2 = RATIONAL ? 1. / (1 + k[5] * r2 + k[6] * r4 + k[7] * r6) : 1.0;
         double xd = (RATIONAL ? x * cdist * icdist2 : x * cdist) + k[2] * a1 + k[3] * a2;
@@ -241,7 +269,7 @@ __device__ __forceinline__ void omni_corner(const double* R, const double* T, co
         Xc[1] = Yr[1] + T[1];
         Xc[2] = Yr[2] + T[2];
         nrm = sqrt(Xc[0] * Xc[0] + Xc[1] * Xc[1] + Xc[2] * Xc[2]);
-        double inrm = 1. / nrm;
+        const double inrm = 1. / nrm;
         Xs[0] = Xc[0] * inrm;
         Xs[1] = Xc[1] * inrm;
         Xs[2] = Xc[2] * inrm;
@@ -250,15 +278,14 @@ __device__ __forceinline__ void omni_corner(const double* R, const double* T, co
         r2 = xu0 * xu0 + xu1 * xu1;
         r4 = r2 * r2;
         const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3];
-        double xd0 = xu0 * (1 + k1 * r2 + k2 * r4) + 2 * p1 * xu0 * xu1 + p2 * (r2 + 2 * xu0 * xu0);
-        double xd1 = xu1 * (1 + k1 * r2 + k2 * r4) + p1 * (r2 + 2 * xu1 * xu1) + 2 * p2 * xu0 * xu1;
+        const double xd0 = xu0 * (1 + k1 * r2 + k2 * r4) + 2 * p1 * xu0 * xu1 + p2 * (r2 + 2 * xu0 * xu0);
+        const double xd1 = xu1 * (1 + k1 * r2 + k2 * r4) + p1 * (r2 + 2 * xu1 * xu1) + 2 * p2 * xu0 * xu1;
         u = (float)(f0 * xd0 + s * xd1 + c0);
         v = (float)(f1 * xd1 + c1);
     }
     const double k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3];
     const double r_1 = 1.0 / nrm, r_3 = r_1 * r_1 * r_1;
     const double den = 1.0 / (Xs[2] + xi);
-    // dxu/dXs (2x3)
     const double a00 = den, a02 = -Xs[0] * den * den, a11 = den, a12 = -Xs[1] * den * den;
     const double t1 = 2 * k1 * xu0 + 4 * k2 * xu0 * r2;
     const double t2 = 2 * k1 * xu1 + 4 * k2 * xu1 * r2;
@@ -266,13 +293,10 @@ __device__ __forceinline__ void omni_corner(const double* R, const double* T, co
     const double b01 = 2 * p1 * xu0 + 2 * p2 * xu1 + xu0 * t2;
     const double b10 = 2 * p1 * xu0 + 2 * p2 * xu1 + xu1 * t1;
     const double b11 = k2 * r4 + 2 * p2 * xu0 + 6 * p1 * xu1 + xu1 * t2 + k1 * r2 + 1;
-    // P = dxpd/dxd * dxd/dxu (2x2)
     const double q00 = f0 * b00 + s * b10, q01 = f0 * b01 + s * b11;
     const double q10 = f1 * b10, q11 = f1 * b11;
-    // Q = P * dxu/dXs (2x3)
     const double w00 = q00 * a00, w01 = q01 * a11, w02 = q00 * a02 + q01 * a12;
     const double w10 = q10 * a00, w11 = q11 * a11, w12 = q10 * a02 + q11 * a12;
-    // D = Q * dXs/dXc,  dXs/dXc = r_1 I - r_3 Xc Xc^T
     const double d0 = w00 * Xc[0] + w01 * Xc[1] + w02 * Xc[2];
     const double d1 = w10 * Xc[0] + w11 * Xc[1] + w12 * Xc[2];
     D[0] = w00 * r_1 - d0 * r_3 * Xc[0];
@@ -283,21 +307,119 @@ __device__ __forceinline__ void omni_corner(const double* R, const double* T, co
     D[5] = w12 * r_1 - d1 * r_3 * Xc[2];
 }
 
+// ---------------------------------------------------------------- photo back-substitution
+// dp = L^-T (z - sum_e Y_e^T dg_e) for one photo (one thread); used by k_backsub.
+__device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gblock, const double* Y,
+                                           const double* Lp, const double* zp, const double* dg, int p,
+                                           double t[6]) {
+    const double* z = zp + 6 * (size_t)p;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) t[k] = z[k];
+    for (int e = photo_ptr[p]; e < photo_ptr[p + 1]; ++e) {
+        const int g = gblock[e];
+        if (g < 0) continue;
+        const double* Ye = Y + 36 * (size_t)e;
+        const double* d = dg + 6 * g;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) s += Ye[i * 6 + k] * d[i];
+            t[k] -= s;
+        }
+    }
+    const double* Lm = Lp + 36 * (size_t)p;
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+        double s = t[i];
+#pragma unroll
+        for (int k = i + 1; k < 6; ++k) s -= Lm[k * 6 + i] * t[k];
+        t[i] = s / Lm[i * 6 + i];
+    }
+}
+
 // ---------------------------------------------------------------- k_linearize
+// Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
+#ifdef MCC_DIAG
+#define STAMP(k)                                                                                   \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && a.stamps) {                                                        \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            a.stamps[16 * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memtime();     \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+        }                                                                                          \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
 template <int MODEL, bool RATIONAL, bool PRISM>
 __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
-    if (a.state->done) return;
+    State* st = a.state;
+    if (st->done) return;
+    STAMP(0);
     const int photo = blockIdx.x;
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
-    double* ph = smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double));   // photo scratch
+    double* ph = smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double));
+    double* xp = ph;          // 6  photo params (double of the float32 state)
+    double* tk = ph + 6;      // 6
+    double* Hs = ph + 12;     // 36
+    double* gs = ph + 48;     // 6
+    double* Lm = ph + 54;     // 36 (lower)
+    double* z = ph + 90;      // 6
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float* xg = a.x + a.global_dim + 6 * (size_t)photo;
+
+    // ---- phase 0: pending update of the previous step (fused back-substitution)
+    const int pending = st->pending;
+    if (pending) {
+        if (tid < 6) {
+            const int k = tid;
+            double s = a.zp[6 * (size_t)photo + k];
+            for (int le = 0; le < ne; ++le) {
+                const int g = a.gblock[e0 + le];
+                if (g < 0) continue;
+                const double* Ye = a.Y + 36 * (size_t)(e0 + le);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) s -= Ye[i * 6 + k] * a.dg[6 * g + i];
+            }
+            tk[k] = s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const double* Lo = a.Lp + 36 * (size_t)photo;
+            double t[6];
+            for (int k = 0; k < 6; ++k) t[k] = tk[k];
+            for (int i = 5; i >= 0; --i) {
+                double s = t[i];
+                for (int k = i + 1; k < 6; ++k) s -= Lo[k * 6 + i] * t[k];
+                t[i] = s / Lo[i * 6 + i];
+            }
+            const double alpha = st->alpha;
+            double g2 = 0.0, x2 = 0.0;
+            for (int k = 0; k < 6; ++k) {
+                const float G = (float)(alpha * t[k]);     // G = alpha*delta -> CV_32F (:491-496)
+                const float xn = xg[k] + G;                // x = x + G (:501)
+                xg[k] = xn;
+                xp[k] = xn;
+                g2 += (double)G * (double)G;
+                x2 += (double)xn * (double)xn;
+            }
+            a.photo_norm[2 * (size_t)photo] = g2;
+            a.photo_norm[2 * (size_t)photo + 1] = x2;
+        }
+    } else if (tid < 6) {
+        xp[tid] = xg[tid];
+    }
+    __syncthreads();
+    STAMP(1);
 
     // ---- phase A: edge prologues, one lane per edge
-    for (int le = tid; le < ne; le += blockDim.x) edge_prologue<MODEL>(a, photo, e0 + le, el[le]);
+    for (int le = tid; le < ne; le += blockDim.x) edge_prologue<MODEL>(a, xp, e0 + le, el[le]);
     __syncthreads();
+    STAMP(2);
 
     // ---- phase B/C: corner sweep + reduction + chain products, one wave per edge
     for (int base = 0; base < ne; base += 4) {
@@ -329,11 +451,10 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
                     omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
                 else
                     pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
-                const float euf = ou - u, evf = ov - v;
+                const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
                 if (a.resid) { a.resid[2 * c] = euf; a.resid[2 * c + 1] = evf; }
                 const double eu = euf, ev = evf;
-                // J' rows: [Y x d, d]
-                double ju[6], jv[6];
+                double ju[6], jv[6];   // J' rows: [Y x d, d]
                 ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
                 ju[1] = Yr[2] * D[0] - Yr[0] * D[2];
                 ju[2] = Yr[0] * D[1] - Yr[1] * D[0];
@@ -350,6 +471,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
 #pragma unroll
                 for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
             }
+            if (wave == 0) STAMP(3);
             const double sum = wave_reduce_scatter32(acc, lane);
             const int idx = bfly_index(lane);
             if ((lane & 1) == 0 && idx < 27) {
@@ -365,8 +487,8 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
             }
         }
         __syncthreads();
-        // X = A' G  (A' symmetric)
-        if (le < ne) {
+        STAMP(4);
+        if (le < ne) {   // X = A' G  (A' symmetric)
             EdgeLds& L = el[le];
             for (int t = lane; t < 72; t += 64) {
                 const int w = t / 36, ij = t % 36, i = ij / 6, j = ij % 6;
@@ -378,8 +500,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
             }
         }
         __syncthreads();
-        // H = G^T X, g = G^T b'
-        if (le < ne) {
+        if (le < ne) {   // H = G^T X, g = G^T b'
             EdgeLds& L = el[le];
             for (int t = lane; t < 120; t += 64) {
                 if (t < 108) {
@@ -404,10 +525,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
     }
 
     // ---- phase D: photo block: Hpp = sum_e, Cholesky, z = L^-1 gp, Y_e = Hgp_e L^-T
-    double* Hs = ph;        // 36
-    double* gs = ph + 36;   // 6
-    double* Lm = ph + 48;   // 36 (lower)
-    double* z = ph + 84;    // 6
+    STAMP(5);
     if (tid < 42) {
         double s = 0.0;
         for (int le = 0; le < ne; ++le) s += tid < 36 ? el[le].Hpp[tid] : el[le].gp[tid - 36];
@@ -434,14 +552,13 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
             for (int k = 0; k < i; ++k) s -= Lm[i * 6 + k] * z[k];
             z[i] = s / Lm[i * 6 + i];
         }
-        if (!ok) atomicOr(&a.state->error, 1);
+        if (!ok) atomicOr(&st->error, 1);
     }
     __syncthreads();
-    double* Lg = a.Lp + 36 * (size_t)photo;
-    if (tid < 36) Lg[tid] = Lm[tid];
+    STAMP(6);
+    if (tid < 36) a.Lp[36 * (size_t)photo + tid] = Lm[tid];
     else if (tid < 42) a.zp[6 * (size_t)photo + tid - 36] = z[tid - 36];
     else if (tid < 48) a.gp_tot[6 * (size_t)photo + tid - 42] = gs[tid - 42];
-    // Y rows: (edge, row i of Hgp) -> forward substitution with L
     for (int t = tid; t < 6 * ne; t += blockDim.x) {
         const int le = t / 6, i = t % 6;
         const EdgeLds& L = el[le];
@@ -457,120 +574,260 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
             for (int j = 0; j < 6; ++j) y[j] = 0.0;
         }
         double* Yo = a.Y + 36 * (size_t)e + 6 * i;
-        for (int j = 0; j < 6; ++j) Yo[j] = y[j];
         double* Ho = a.Hgg + 36 * (size_t)e + 6 * i;
-        for (int j = 0; j < 6; ++j) Ho[j] = L.has_global ? L.Hgg[i * 6 + j] : 0.0;
+        for (int j = 0; j < 6; ++j) {
+            Yo[j] = y[j];
+            Ho[j] = L.has_global ? L.Hgg[i * 6 + j] : 0.0;
+        }
         a.gg[6 * (size_t)e + i] = L.has_global ? L.gg[i] : 0.0;
     }
-}
-
-// ---------------------------------------------------------------- k_schur
-// Work item: pairs [begin, end) of one camera-pair block (gb1, gb2).  Thread t < 252:
-// entry q = t % 42 (0..35: S block entry, 36..41: r entry), chunk = t / 42 (6 chunks).
-__global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
-    if (a.state->done) return;
-    const int item = blockIdx.x;
-    const int4 it = a.items[item];   // {block, begin, end, diag}
-    __shared__ double part[6][42];
-    const int tid = threadIdx.x;
-    const int q = tid % 42, chunk = tid / 42;
-    double s = 0.0;
-    if (chunk < 6) {
-        for (int p = it.y + chunk; p < it.z; p += 6) {
-            const int4 pr = a.pairs[p];   // {e1, e2, photo, self}
-            const double* Y1 = a.Y + 36 * (size_t)pr.x;
-            if (q < 36) {
-                const int i = q / 6, j = q % 6;
-                const double* Y2 = a.Y + 36 * (size_t)pr.y;
-                double t = 0.0;
-#pragma unroll
-                for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * Y2[j * 6 + k];
-                s -= t;
-                if (pr.w) s += a.Hgg[36 * (size_t)pr.x + q];
-            } else if (pr.w) {
-                const int i = q - 36;
-                const double* zp = a.zp + 6 * (size_t)pr.z;
-                double t = 0.0;
-#pragma unroll
-                for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * zp[k];
-                s += a.gg[6 * (size_t)pr.x + i] - t;
-            }
-        }
-        part[chunk][q] = s;
-    }
+#ifdef MCC_DIAG
     __syncthreads();
-    if (tid < 42) {
-        double t = part[0][tid];
-        for (int c = 1; c < 6; ++c) t += part[c][tid];
-        a.item_out[42 * (size_t)item + tid] = t;
-    }
+    STAMP(7);
+#endif
 }
 
-// ---------------------------------------------------------------- k_assemble (1 workgroup)
-// packed layout: [S upper triangle m(m+1)/2][r m][jte_g m][normG2][normX2]
-__global__ __launch_bounds__(256) void k_assemble(AsmArgs a) {
-    if (a.state->done) return;
-    const int m = a.m, nb = m / 6;
-    const int tid = threadIdx.x;
-    const int ntri = m * (m + 1) / 2;
-    for (int t = tid; t < ntri + 2 * m + 2; t += blockDim.x) {
-        double v = 0.0;
-        if (t < ntri) {
-            // (i, j) with i <= j from packed index
-            int i = 0, rem = t;
-            while (rem >= m - i) { rem -= m - i; ++i; }
-            const int j = i + rem;
-            int b1 = i / 6, b2 = j / 6, ii = i % 6, jj = j % 6;
-            const int blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
-            for (int k = a.block_items[blk]; k < a.block_items[blk + 1]; ++k)
-                v += a.item_out[42 * (size_t)k + ii * 6 + jj];
-        } else if (t < ntri + m) {
-            const int g = t - ntri, b = g / 6;
-            const int blk = b * nb - b * (b - 1) / 2;
-            for (int k = a.block_items[blk]; k < a.block_items[blk + 1]; ++k)
-                v += a.item_out[42 * (size_t)k + 36 + g % 6];
-        } else if (t < ntri + 2 * m) {
-            // JTE of the global block: sum over edges of gg (edge order = photo-major)
-            const int g = t - ntri - m, b = g / 6;
-            for (int k = a.gblock_ptr[b]; k < a.gblock_ptr[b + 1]; ++k)
-                v += a.gg[6 * (size_t)a.gblock_edges[k] + g % 6];
-        } else {
-            const int w = t - ntri - 2 * m;   // 0: normG2, 1: normX2 (partials of the last update)
-            if (a.state->iter > 0) {
-                for (int p = 0; p < a.n_photos; ++p) v += a.photo_norm[2 * p + w];
-                if (a.rank == 0) v += w ? a.state->cam_normX2 : a.state->cam_normG2;
-            }
-        }
-        a.packed[t] = v;
-    }
+// ---------------------------------------------------------------- global solve (one workgroup)
+// Stop test (src/multicalib.cpp:475-477), Cholesky of S (m <= 128, Crout, rows spread over the
+// 256 threads, one barrier per column), triangular solves (one wavefront, shuffle dot
+// products), global-block delta and float32 update.  S (m x m, overwritten by L in its lower
+// triangle) and r (m) are in LDS.
+__device__ __forceinline__ double sub_sum(double v, int tpr) {
+    for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
+    return v;
 }
 
-// ---------------------------------------------------------------- k_solve (1 workgroup)
-// Stop test, Cholesky of S (one wavefront, LDS), global-block solve and float32 update.
-__global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
+__device__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
     State* st = a.state;
-    if (st->done) return;
     const int m = a.m, tid = threadIdx.x;
-    const int ntri = m * (m + 1) / 2;
-    extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* S = sm;            // m*m
-    double* r = sm + m * m;    // m
     __shared__ int stop;
     if (tid == 0) {
         const int k = st->iter;
         double change = 1.0;
-        if (k > 0) change = sqrt(a.packed[ntri + 2 * m]) / sqrt(a.packed[ntri + 2 * m + 1]);
-        if (k > 0) st->change = change;
+        if (k > 0) {
+            change = sqrt(normG2) / sqrt(normX2);   // change = norm(G) / norm(x) (:504)
+            st->change = change;
+        }
         const int ty = st->crit_type;
         int s = (ty == 1 && k >= st->max_count) || (ty == 2 && change <= st->eps) ||
                 (ty == 3 && (change <= st->eps || k >= st->max_count));
         if (!a.do_update) s = 0;
         stop = s;
         if (s) st->done = 1;
+        st->pending = 0;   // this step's k_linearize has applied the previous update
         st->alpha = a.do_update ? (k < a.n_alpha ? a.alpha[k] : pow(0.95, (double)k + 1.0)) : 0.0;
     }
     __syncthreads();
     if (stop) return;
+    // ---- Crout: L[i][j] = (S[i][j] - sum_{k<j} L[i][k] L[j][k]) / L[j][j]
+    const int tpr = m <= 32 ? 8 : (m <= 64 ? 4 : 2);   // threads per row (same wavefront)
+    const int row = tid / tpr, sub = tid % tpr;
+    for (int j = 0; j < m; ++j) {
+        double dj = 0.0, di = 0.0;
+        const bool act = row < m && row >= j;
+        if (act) {
+            for (int k = sub; k < j; k += tpr) {
+                const double ljk = S[j * m + k];
+                dj += ljk * ljk;
+                di += S[row * m + k] * ljk;
+            }
+        }
+        dj = sub_sum(dj, tpr);
+        di = sub_sum(di, tpr);
+        if (act && sub == 0) {
+            double d = S[j * m + j] - dj;
+            if (!(d > 0.0)) {
+                if (row == j) atomicOr(&st->error, 2);
+                d = 1.0;
+            }
+            const double l = sqrt(d);
+            if (row == j) S[j * m + j] = l;
+            else S[row * m + j] = (S[row * m + j] - di) / l;
+        }
+        __syncthreads();
+    }
+    // ---- L y = r, L^T x = y (one wavefront; lanes split the dot products)
+    if (tid < 64) {
+        const int lane = tid;
+        for (int j = 0; j < m; ++j) {
+            double s = 0.0;
+            for (int k = lane; k < j; k += 64) s += S[j * m + k] * r[k];
+            s = wave_sum(s);
+            const double yj = (r[j] - s) / S[j * m + j];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == 0) r[j] = yj;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        for (int j = m - 1; j >= 0; --j) {
+            double s = 0.0;
+            for (int k = j + 1 + lane; k < m; k += 64) s += S[k * m + j] * r[k];
+            s = wave_sum(s);
+            const double xj = (r[j] - s) / S[j * m + j];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == 0) r[j] = xj;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
+        // global block: delta, update, norm partials (identical on every rank)
+        const double alpha = st->alpha;
+        double g2 = 0.0, x2 = 0.0;
+        for (int i = lane; i < m; i += 64) {
+            const double d = r[i];
+            a.dg[i] = d;
+            a.delta[i] = d;
+            if (a.do_update) {
+                const float G = (float)(alpha * d);   // G = alpha*delta -> CV_32F (:491-496)
+                const float xn = a.x[i] + G;          // x = x + G (:501)
+                a.x[i] = xn;
+                g2 += (double)G * (double)G;
+                x2 += (double)xn * (double)xn;
+            }
+        }
+        g2 = wave_sum(g2);
+        x2 = wave_sum(x2);
+        if (lane == 0 && a.do_update) {
+            st->cam_normG2 = g2;
+            st->cam_normX2 = x2;
+            st->iter = st->iter + 1;
+            st->pending = 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- k_schur
+// Work item: pairs [begin, end) of one camera-pair block.  Thread t < 240: entry q = t % 48
+// (0..35: S entry, 36..41: r entry, 42..47: JTE of the global block), sub-chunk s = t / 48.
+// Norm items sum 256 photos' norm partials.  The last workgroup to finish assembles the packed
+// system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2] in fixed order, and with
+// fuse_solve (single GPU) solves it in place.
+constexpr int kSub = 5;
+__global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
+    State* st = a.state;
+    if (st->done) return;
+    const int item = blockIdx.x;
+    const int tid = threadIdx.x;
+    __shared__ double part[kSub][48];
+    __shared__ double red[256];
+    __shared__ int last;
+    if (item < a.n_items) {
+        const int4 it = a.items[item];   // {block, begin, end, -}
+        const int q = tid % 48, sub = tid / 48;
+        double s = 0.0;
+        if (sub < kSub) {
+            for (int p = it.y + sub; p < it.z; p += kSub) {
+                const int4 pr = a.pairs[p];   // {e1, e2, photo, self}
+                const double* Y1 = a.Y + 36 * (size_t)pr.x;
+                if (q < 36) {
+                    const int i = q / 6, j = q % 6;
+                    const double* Y2 = a.Y + 36 * (size_t)pr.y;
+                    double t = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * Y2[j * 6 + k];
+                    s -= t;
+                    if (pr.w) s += a.Hgg[36 * (size_t)pr.x + q];
+                } else if (pr.w) {
+                    const int i = (q - 36) % 6;
+                    const double gi = a.gg[6 * (size_t)pr.x + i];
+                    if (q < 42) {
+                        const double* zp = a.zp + 6 * (size_t)pr.z;
+                        double t = 0.0;
+#pragma unroll
+                        for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * zp[k];
+                        s += gi - t;
+                    } else {
+                        s += gi;
+                    }
+                }
+            }
+            part[sub][q] = s;
+        }
+        __syncthreads();
+        if (tid < 48) {
+            double t = part[0][tid];
+            for (int c = 1; c < kSub; ++c) t += part[c][tid];
+            a.item_out[48 * (size_t)item + tid] = t;
+        }
+    } else {
+        const int c = item - a.n_items;
+        const int p = c * 256 + tid;
+        for (int w = 0; w < 2; ++w) {
+            red[tid] = p < a.n_photos ? a.photo_norm[2 * (size_t)p + w] : 0.0;
+            __syncthreads();
+            for (int o = 128; o >= 1; o >>= 1) {
+                if (tid < o) red[tid] += red[tid + o];
+                __syncthreads();
+            }
+            if (tid == 0) a.item_out[48 * (size_t)item + w] = red[0];
+            __syncthreads();
+        }
+    }
+    // ---- publish the partial, take a ticket (agent-scope release/acquire, cdna guide G16)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == (int)gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // ---- assemble (fixed order): S full into LDS, packed to global
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    double* S = sm;          // m*m
+    double* r = sm + m * m;  // m
+    __shared__ double norms[2];
+    for (int t = tid; t < m * m + 2 * m + 2; t += blockDim.x) {
+        double v = 0.0;
+        if (t < m * m) {
+            const int i = t / m, j = t % m;
+            if (j < i) continue;
+            const int b1 = i / 6, b2 = j / 6, ii = i % 6, jj = j % 6;
+            const int blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
+            const int k0 = a.block_items[blk], k1 = a.block_items[blk + 1];
+            const double* src = a.item_out + ii * 6 + jj;
+#pragma unroll 8
+            for (int k = k0; k < k1; ++k) v += src[48 * (size_t)k];
+            S[i * m + j] = v;
+            S[j * m + i] = v;
+            a.packed[i * m - i * (i - 1) / 2 + (j - i)] = v;
+        } else if (t < m * m + 2 * m) {
+            const int u = t - m * m, g = u % m, w = u / m, b = g / 6;
+            const int blk = b * nb - b * (b - 1) / 2;
+            const int k0 = a.block_items[blk], k1 = a.block_items[blk + 1];
+            const double* src = a.item_out + 36 + 6 * w + g % 6;
+#pragma unroll 8
+            for (int k = k0; k < k1; ++k) v += src[48 * (size_t)k];
+            if (w == 0) r[g] = v;
+            a.packed[ntri + u] = v;
+        } else {
+            const int w = t - m * m - 2 * m;   // 0: normG2, 1: normX2 of the last update
+            if (st->iter > 0) {
+                for (int k = a.n_items; k < (int)gridDim.x; ++k) v += a.item_out[48 * (size_t)k + w];
+                if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
+            }
+            norms[w] = v;
+            a.packed[ntri + 2 * m + w] = v;
+        }
+    }
+    if (!a.fuse_solve) return;
+    __syncthreads();
+    solve_global(a.solve, S, r, norms[0], norms[1]);
+}
+
+// ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)
+__global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
+    if (a.ctx.state->done) return;
+    const int m = a.ctx.m, tid = threadIdx.x, ntri = m * (m + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* S = sm;
+    double* r = sm + m * m;
     for (int t = tid; t < ntri; t += blockDim.x) {
         int i = 0, rem = t;
         while (rem >= m - i) { rem -= m - i; ++i; }
@@ -581,99 +838,20 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     }
     for (int t = tid; t < m; t += blockDim.x) r[t] = a.packed[ntri + t];
     __syncthreads();
-    if (tid < 64) {
-        const int lane = tid;
-        // right-looking Cholesky, lower triangle, one wavefront (LDS ops of one wave are ordered)
-        for (int j = 0; j < m; ++j) {
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            const double d = S[j * m + j];
-            if (!(d > 0.0) && lane == 0) atomicOr(&st->error, 2);
-            const double l = sqrt(d > 0.0 ? d : 1.0), il = 1.0 / l;
-            for (int i = j + 1 + lane; i < m; i += 64) S[i * m + j] *= il;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane == 0) S[j * m + j] = l;
-            // trailing update of the lower triangle
-            const int w = m - j - 1;
-            for (int t = lane; t < w * (w + 1) / 2; t += 64) {
-                int ii = 0, rem = t;
-                while (rem > ii) { rem -= ii + 1; ++ii; }
-                const int i = j + 1 + ii, k = j + 1 + rem;
-                S[i * m + k] -= S[i * m + j] * S[k * m + j];
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane == 0) {
-            for (int i = 0; i < m; ++i) {
-                double s = r[i];
-                for (int k = 0; k < i; ++k) s -= S[i * m + k] * r[k];
-                r[i] = s / S[i * m + i];
-            }
-            for (int i = m - 1; i >= 0; --i) {
-                double s = r[i];
-                for (int k = i + 1; k < m; ++k) s -= S[k * m + i] * r[k];
-                r[i] = s / S[i * m + i];
-            }
-        }
-    }
-    __syncthreads();
-    // global block: delta, update, norm partials (identical on every rank)
-    if (tid == 0) {
-        const double alpha = st->alpha;
-        double g2 = 0.0, x2 = 0.0;
-        for (int i = 0; i < m; ++i) {
-            a.dg[i] = r[i];
-            a.delta[i] = r[i];
-            if (a.do_update) {
-                const float G = (float)(alpha * r[i]);
-                const float xn = a.x[i] + G;
-                a.x[i] = xn;
-                g2 += (double)G * (double)G;
-                x2 += (double)xn * (double)xn;
-            }
-        }
-        if (a.do_update) {
-            st->cam_normG2 = g2;
-            st->cam_normX2 = x2;
-            st->iter = st->iter + 1;
-        }
-    }
+    solve_global(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
 }
 
 // ---------------------------------------------------------------- k_backsub
-// one thread per photo: dp = L^-T (z - sum_e Y_e^T dg_e), x_p = fl32(x_p + fl32(a dp))
+// one thread per photo: dp = L^-T (z - sum_e Y_e^T dg_e); with do_update the float32 update
+// (flush of a pending update), otherwise only deltaX.
 __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
-    const State* st = a.state;
-    if (st->done) return;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n_photos) return;
     double t[6];
-    const double* z = a.zp + 6 * (size_t)p;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) t[k] = z[k];
-    for (int e = a.photo_ptr[p]; e < a.photo_ptr[p + 1]; ++e) {
-        const int g = a.edge_gblock[e];
-        if (g < 0) continue;
-        const double* Y = a.Y + 36 * (size_t)e;
-        const double* dg = a.dg + 6 * g;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) s += Y[i * 6 + k] * dg[i];
-            t[k] -= s;
-        }
-    }
-    const double* Lm = a.Lp + 36 * (size_t)p;
-#pragma unroll
-    for (int i = 5; i >= 0; --i) {
-        double s = t[i];
-#pragma unroll
-        for (int k = i + 1; k < 6; ++k) s -= Lm[k * 6 + i] * t[k];
-        t[i] = s / Lm[i * 6 + i];
-    }
+    photo_delta(a.photo_ptr, a.gblock, a.Y, a.Lp, a.zp, a.dg, p, t);
     const int col = a.m + 6 * p;
+    const double alpha = a.state->alpha;
     double g2 = 0.0, x2 = 0.0;
-    const double alpha = st->alpha;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         a.delta[col + k] = t[k];
@@ -696,10 +874,11 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
 // src/doubleSide.cpp:640-769): float32 Rodrigues + float32 gemm, Rodrigues back, float
 // projection, ferror = sqrtf(ex*ex + ey*ey), per-edge sequential float sum.  One wave per edge.
 __device__ __forceinline__ void rod_f32(const float* r, float* Rf) {
-    double rd[3] = {r[0], r[1], r[2]}, Rd[9];
-    rodrigues_v2m(rd, Rd);
+    double rd[3] = {r[0], r[1], r[2]};
+    Rot o;
+    rodrigues_v2m(rd, o);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Rf[k] = (float)Rd[k];
+    for (int k = 0; k < 9; ++k) Rf[k] = (float)o.R[k];
 }
 
 template <int MODEL, bool RATIONAL, bool PRISM>
@@ -771,14 +950,14 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
                 Tt[i] = (float)((double)t * 1.0 + (double)xc[3 + i] * 1.0);
             }
         }
-        double Rd[9], rv[3];
+        double Rd[9], rv[3], th, s, c;
         for (int k = 0; k < 9; ++k) Rd[k] = Rt[k];
         polar3(Rd);
-        rodrigues_m2v(Rd, rv);
+        rodrigues_m2v(Rd, rv, th, s, c);
         double rf[3] = {(double)(float)rv[0], (double)(float)rv[1], (double)(float)rv[2]};
-        double Rr[9];
-        rodrigues_v2m(rf, Rr);
-        for (int k = 0; k < 9; ++k) Rs[k] = Rr[k];
+        Rot rr;
+        rodrigues_v2m(rf, rr);
+        for (int k = 0; k < 9; ++k) Rs[k] = rr.R[k];
         for (int k = 0; k < 3; ++k) Ts[k] = Tt[k];
     }
     __syncthreads();
@@ -825,8 +1004,10 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
 }
 
 size_t mcc_lin_shmem(int max_edges_per_photo) {
-    return (size_t)max_edges_per_photo * sizeof(EdgeLds) + 96 * sizeof(double);
+    return (size_t)max_edges_per_photo * sizeof(EdgeLds) + kPhotoScratch * sizeof(double);
 }
+
+size_t mcc_solve_shmem(int m) { return (size_t)(m * m + m) * sizeof(double); }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
     const size_t shmem = mcc_lin_shmem(max_epp);
@@ -837,30 +1018,32 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_lin_attrs(int max_epp) {
-    const size_t shmem = mcc_lin_shmem(max_epp);
-    if (shmem <= 64 * 1024) return hipSuccess;
-#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
+hipError_t mcc_set_kernel_attrs(int max_epp, int m) {
     hipError_t err = hipSuccess;
-    for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
-                         SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true), SETA(2, true, true)})
-        if (e != hipSuccess) err = e;
+    const size_t shmem = mcc_lin_shmem(max_epp);
+    if (shmem > 64 * 1024) {
+#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
+        for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
+                             SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true), SETA(2, true, true)})
+            if (e != hipSuccess) err = e;
 #undef SETA
+    }
+    const size_t ss = mcc_solve_shmem(m);
+    if (ss > 60 * 1024) {
+        hipError_t e1 = hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
+        hipError_t e2 = hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
+        if (e1 != hipSuccess) err = e1;
+        if (e2 != hipSuccess) err = e2;
+    }
     return err;
 }
 
-hipError_t mcc_launch_schur(const SchurArgs& a, int n_items, hipStream_t s) {
-    if (n_items > 0) hipLaunchKernelGGL(k_schur, dim3(n_items), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-hipError_t mcc_launch_assemble(const AsmArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_assemble, dim3(1), dim3(256), 0, s, a);
+hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_schur, dim3(grid), dim3(256), mcc_solve_shmem(a.m), s, a);
     return hipGetLastError();
 }
 hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
-    const size_t shmem = (size_t)(a.m * a.m + a.m) * sizeof(double);
-    if (shmem > 64 * 1024) (void)hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), shmem, s, a);
+    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), mcc_solve_shmem(a.ctx.m), s, a);
     return hipGetLastError();
 }
 hipError_t mcc_launch_backsub(const BacksubArgs& a, hipStream_t s) {
