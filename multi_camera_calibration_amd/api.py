@@ -236,10 +236,10 @@ class BundleAdjuster:
 
     def stamps(self):
         """libmcc_diag.so only: first call arms, later calls return [n_photos, 16] s_memtime stamps."""
-        out = np.zeros(16 * max(self.prob.n_photos, 1), np.int64)
+        out = np.zeros(16 * max(self.prob.n_photos, 1) + 8 * 65536, np.int64)
         _check(lib().mcc_debug_stamps(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), out.size),
                "mcc_debug_stamps")
-        return out.reshape(-1, 16)
+        return out
 
     # -- multi-GPU
     def comm_init(self, uid: bytes, nranks: int, rank: int):

@@ -107,6 +107,7 @@ struct mcc_problem {
     int model = 0, C = 0, V = 0, E = 0, nd = 0, m = 0, P = 0, device = 0;
     long long corners = 0;
     bool rational = false, prism = false;
+    int has_back = 0;
     int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
     hipStream_t stream = nullptr;
 
@@ -161,6 +162,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.K = p->K.p; la.D = p->D.p; la.xi = p->xi.p;
     la.cam_rt = p->cam_rt.p; la.ds_rt = p->ds_rt.p;
     la.nd = p->nd; la.global_dim = p->m;
+    la.n_cams = p->C; la.has_back = p->has_back;
     la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.gg = p->gg.p; la.Lp = p->Lp.p; la.zp = p->zp.p;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
@@ -184,6 +186,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.packed = p->packed.p;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = multi ? 0 : 1;
     sa.solve = solve_ctx(p, do_update);
+    sa.stamps = p->stamps.p ? p->stamps.p + 16 * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
     if (multi) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
@@ -374,6 +377,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             p->dev2ref_corner[off + i] = s;
         }
         info[de] = make_int4(d->edge_cam[e], side, (int)off, n);
+        if (side == MCC_BACK) p->has_back = 1;
         ephoto[de] = d->edge_photo[e];
         p->edge_n_dev[de] = n;
         if (d->model == MCC_MODEL_DOUBLESIDE) gblock[de] = side == MCC_BACK ? 0 : -1;
@@ -460,8 +464,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E)); HIPC(p->Hgg.alloc(36 * (size_t)E)); HIPC(p->gg.alloc(6 * (size_t)E));
-    HIPC(p->Lp.alloc(36 * (size_t)V)); HIPC(p->zp.alloc(6 * (size_t)V)); HIPC(p->gp_tot.alloc(6 * (size_t)V));
-    HIPC(p->item_out.alloc(48 * (size_t)(items.size() + p->n_norm_chunks)));
+    HIPC(p->Lp.alloc(42 * (size_t)V));   // L + 1/L_ii per photo
+    HIPC(p->zp.alloc(6 * (size_t)V));
+    HIPC(p->gp_tot.alloc(6 * (size_t)V));
+    // + 24 zeroed items of padding: the assembly loads a fixed 24 items per block unconditionally
+    HIPC(p->item_out.alloc(48 * (size_t)(items.size() + p->n_norm_chunks + 24)));
+    HIPC(hipMemset(p->item_out.p, 0, sizeof(double) * p->item_out.n));
     HIPC(p->counter.alloc(1));
     HIPC(hipMemset(p->counter.p, 0, sizeof(int)));
     p->ntri = p->m * (p->m + 1) / 2;
@@ -476,8 +484,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     std::memset(p->h_state, 0, sizeof(State));
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, p->m));
-    if (mcc_lin_shmem(p->max_epp) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
+    if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
+    if (mcc_lin_shmem(p->max_epp, C) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -512,7 +521,10 @@ int mcc_set_params(mcc_problem* p, const float* x, int n) {
     HIPCHK(hipSetDevice(p->device));
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->x.p, x, sizeof(float) * n, hipMemcpyHostToDevice));
-    const int zero = 0;   // the new x supersedes any pending photo update
+    // new parameters start a new optimisation: iteration 0 (alpha = 0.95^1), no pending update
+    int rc = set_state(p, 1, 0, 0, 0.0);
+    if (rc) return rc;
+    const int zero = 0;
     HIPCHK(hipMemcpy(&p->state.p->pending, &zero, sizeof(int), hipMemcpyHostToDevice));
     return MCC_OK;
 }
@@ -637,12 +649,15 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     if (!p->stamps.p) {
-        HIPCHK(p->stamps.alloc(16 * (size_t)std::max(p->V, 1)));
-        HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * 16 * std::max(p->V, 1)));
-        return MCC_OK;   // armed: the next linearisations record
+        const size_t n_st = 16 * (size_t)std::max(p->V, 1) + 8 * (size_t)(p->n_items + p->n_norm_chunks);
+        HIPCHK(p->stamps.alloc(n_st));
+        HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
+        for (auto& g : p->gexec)
+            if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }   // graphs captured the old pointer
+        return MCC_OK;   // armed: the next steps record
     }
     HIPCHK(hipStreamSynchronize(p->stream));
-    const int cnt = std::min(n, 16 * p->V);
+    const int cnt = std::min(n, (int)p->stamps.n);
     HIPCHK(hipMemcpy(out, p->stamps.p, sizeof(long long) * cnt, hipMemcpyDeviceToHost));
     return MCC_OK;
 #else

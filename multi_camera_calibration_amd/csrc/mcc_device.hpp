@@ -159,13 +159,17 @@ __device__ __forceinline__ void polar3(double* R) {
 //   B2 = d T3/d om2 = -[R2 T1]x Jl(om2);   d T3/d T1 = R2, d T3/d T2 = I, other blocks 0.
 // r1 / r2 are the Rodrigues of om1 / om2 (with trig); Jr1 = Jr(om1), Jl2 = Jl(om2).
 struct Motion {
-    double om[3], T[3];
+    double om[3], T[3], R[9];
     double A1[9], A2[9], B2[9];
 };
 
-__device__ __forceinline__ void compose(const double* R1, const double Jr1[9], const double T1[3],
-                                        const double* R2, const double Jl2[9], const double T2[3], Motion& m) {
-    double R3[9], q[3];
+// th / s / c: the composed angle's trig from the matrix -> vector formula (for Jacobians and
+// the Rodrigues of the float32-rounded vector).
+__device__ __forceinline__ void compose(const double* R1, const double* Jr1, const double* T1,
+                                        const double* R2, const double* Jl2, const double* T2, Motion& m,
+                                        double& th, double& s, double& c) {
+    double* R3 = m.R;
+    double q[3];
     {
 #pragma clang fp contract(off)
 #pragma unroll
@@ -177,7 +181,7 @@ __device__ __forceinline__ void compose(const double* R1, const double Jr1[9], c
             m.T[i] = q[i] + T2[i];
         }
     }
-    double th, s, c, Ji[9];
+    double Ji[9];
     rodrigues_m2v(R3, m.om, th, s, c);
     so3_jac_inv(m.om, th, s, c, -1.0, Ji);   // Jr^-1(om3)
     mat3_mul(Ji, Jr1, m.A1);

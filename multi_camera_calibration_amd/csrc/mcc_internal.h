@@ -31,12 +31,12 @@ struct LinArgs {
     const float* K; const float* D; const float* xi;
     const float* cam_rt;      // DOUBLESIDE fixed cameras (rvec, tvec) [6C]
     const double* ds_rt;      // PINHOLE doubleSideTransform (rvec, tvec) [6]
-    int nd, global_dim;
+    int nd, global_dim, n_cams, has_back;
     // outputs
     double* Y;        // [36E] Schur factors Hgp_e L_p^-T
     double* Hgg;      // [36E]
     double* gg;       // [6E]
-    double* Lp;       // [36V]
+    double* Lp;       // [42V] L (6x6 lower) + 1/L_ii
     double* zp;       // [6V]
     double* gp_tot;   // [6V] photo JTE
     float* resid;     // optional [2*corners] float32 residuals (debug)
@@ -54,6 +54,7 @@ struct SolveCtx {
     double* dg;       // [m]
     double* delta;    // [P]
     int m, do_update;
+    long long* stamps;   // MCC_DIAG: solve phase stamps (set by k_schur's last arriver)
 };
 
 struct SchurArgs {
@@ -69,6 +70,7 @@ struct SchurArgs {
     double* packed;
     int m, rank, fuse_solve;
     SolveCtx solve;
+    long long* stamps;   // MCC_DIAG builds: [8 * grid]
 };
 
 struct SolveArgs {
@@ -102,9 +104,9 @@ struct ErrArgs {
 }  // namespace mcc
 
 // launch wrappers (mcc_kernels.hip)
-size_t mcc_lin_shmem(int max_edges_per_photo);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int m);
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);

@@ -22,6 +22,22 @@
 
 namespace mcc {
 
+// ---------------------------------------------------------------- diagnostic stamps
+// Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
+#ifdef MCC_DIAG
+#define STAMPP(ptr, stride, k)                                                                     \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && (ptr)) {                                                           \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            (ptr)[(stride) * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memtime();  \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+        }                                                                                          \
+    } while (0)
+#else
+#define STAMPP(ptr, stride, k) do { } while (0)
+#endif
+#define STAMP(k) STAMPP(a.stamps, 16, k)
+
 // ---------------------------------------------------------------- wave reduction
 // Reduce-scatter butterfly of 32 per-lane doubles across the 64 lanes: 32 shuffles of 64-bit
 // values instead of 6*27.  Afterwards lane l (and l^1) holds the full sum of value index
@@ -55,6 +71,8 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+constexpr int kLpStride = 42;   // per photo: L (6x6, lower) + 1/L_ii
+
 // ---------------------------------------------------------------- per-edge LDS record
 struct EdgeLds {
     double R[9];      // Rodrigues(fl32(om)) used by the projection
@@ -72,7 +90,6 @@ struct EdgeLds {
     int has_global, edge, pad0, pad1;
 };
 static_assert(sizeof(EdgeLds) % 16 == 0, "EdgeLds alignment");
-constexpr int kPhotoScratch = 96;   // doubles after the edge records
 
 // G (6x6) = [[Grr, 0], [Gtr, Gtt]]; Gtt == nullptr means identity.
 __device__ __forceinline__ void store_G(double* G, const double* Grr, const double* Gtr, const double* Gtt) {
@@ -89,113 +106,140 @@ __device__ __forceinline__ void store_G(double* G, const double* Grr, const doub
 // compose_motion(photo, camera) [+ compose_motion(ds, photofront) for BACK edges], float32
 // composed pose, Rodrigues of it for the projection, and the chain maps G = blockdiag(Jl, I) M.
 // src/mymulticalib.cpp:468-614 (pinhole), src/multicalib.cpp:717-824 (omni),
-// src/doubleSide.cpp:288-430 (double side).
-template <int MODEL>
-__device__ void edge_prologue(const LinArgs& a, const double* xp, int e, EdgeLds& L) {
-    const int4 info = a.edge_info[e];
-    const int cam = info.x, side = info.y;
-    double om1[3] = {xp[0], xp[1], xp[2]}, T1[3] = {xp[3], xp[4], xp[5]};
-    double om2[3], T2[3];
-    if (MODEL == MCC_MODEL_DOUBLESIDE) {
+// src/doubleSide.cpp:288-430 (double side).  Rodrigues matrices and Jacobians of the photo, the
+// cameras and the double-side transform come from the workgroup's LDS tables (phase 0).
+struct PhotoLds {
+    double xp[6];        // photo parameters (double of the float32 state)
+    double R1[9], Jr1[9];
+    double Rds[9], Jrds[9], dst[3], pad0;
+    double Lo[42], zo[6], tk[6];     // pending-update staging (L, 1/L_ii, z)
+    double Hs[36], gs[6], Lm[36], z[6], il[6];
+    double dg[128];      // global-block delta of the previous solve
+    // followed by the camera table: [C][18] = {R (9), Jl (9)}
+};
+static_assert(sizeof(PhotoLds) % 16 == 0, "PhotoLds alignment");
+
+// the tail of cvRodrigues2 vector -> matrix given theta, sin, cos (OpenCV order, no contraction)
+__device__ __forceinline__ void rodrigues_formula(const double* r, double th, double sn, double c, double* R) {
+#pragma clang fp contract(off)
+    const double c1 = 1. - c;
+    const double itheta = 1. / th;
+    const double rx = r[0] * itheta, ry = r[1] * itheta, rz = r[2] * itheta;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double r_x[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * cam + k]; T2[k] = a.cam_rt[6 * cam + 3 + k]; }
-    } else if (cam == 0) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
-    } else {
-        const float* xc = a.x + 6 * (cam - 1);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { om2[k] = xc[k]; T2[k] = xc[3 + k]; }
+    for (int k = 0; k < 9; ++k) {
+        const double I = (k == 0 || k == 4 || k == 8) ? 1.0 : 0.0;
+        R[k] = c * I + c1 * rrt[k] + sn * r_x[k];
     }
-    Rot r1, r2;
-    rodrigues_v2m(om1, r1);
-    rodrigues_v2m(om2, r2);
-    double Jr1[9], Jl2[9];
-    so3_jac(om1, r1, -1.0, Jr1);
-    so3_jac(om2, r2, +1.0, Jl2);
-    Motion f;
-    compose(r1.R, Jr1, T1, r2.R, Jl2, T2, f);
-    double om[3], T[3];
-    double GpRR[9], GpTR[9], GgRR[9], GgTR[9];   // pre-Jl blocks (rows 0-2 get Jl applied below)
-    const double* GgTT = nullptr;                // nullptr: identity
-    double Rf[9];
-    int has_global;
-    bool gg_zero = false, gg_tr_zero = false, gp_tr_zero = true;
-    if (side == MCC_BACK) {
-        double dsr[3], dst[3];
-        if (MODEL == MCC_MODEL_DOUBLESIDE) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { dsr[k] = a.x[k]; dst[k] = a.x[3 + k]; }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { dsr[k] = a.ds_rt[k]; dst[k] = a.ds_rt[3 + k]; }
-        }
-        // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506: om2' = front om (FP64)
-        Rot rds, rfr;
-        rodrigues_v2m(dsr, rds);
-        rodrigues_v2m(f.om, rfr);
-        double Jrds[9], Jlf[9];
-        so3_jac(dsr, rds, -1.0, Jrds);
-        so3_jac(f.om, rfr, +1.0, Jlf);
-        Motion b;
-        compose(rds.R, Jrds, dst, rfr.R, Jlf, f.T, b);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { om[k] = b.om[k]; T[k] = b.T[k]; }
-        // photo: E2 * D1 = [[A2b A1, 0], [B2b A1, R2]]   (src/mymulticalib.cpp:509-512)
-        mat3_mul(b.A2, f.A1, GpRR);
-        mat3_mul(b.B2, f.A1, GpTR);
-        gp_tr_zero = false;
-        if (MODEL == MCC_MODEL_DOUBLESIDE) {
-            // ds block: [[A1b, 0], [0, R_front]]  (src/doubleSide.cpp:398-399)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) { GgRR[k] = b.A1[k]; Rf[k] = rfr.R[k]; }
-            GgTT = Rf;
-            gg_tr_zero = true;
-            has_global = 1;
-        } else {
-            // camera block as the reference chains it (src/mymulticalib.cpp:514-517), which
-            // omits dTt/dTf * dTf/dRc at :516 (hazard A12): [[A2b A2, 0], [B2b A2, I]]
-            mat3_mul(b.A2, f.A2, GgRR);
-            mat3_mul(b.B2, f.A2, GgTR);
-            has_global = cam != 0;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { om[k] = f.om[k]; T[k] = f.T[k]; }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) GpRR[k] = f.A1[k];
-        if (MODEL == MCC_MODEL_DOUBLESIDE) {
-            gg_zero = true;   // zero double-side jacobian on the front side (doubleSide.cpp:335-336)
-            has_global = 0;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) { GgRR[k] = f.A2[k]; GgTR[k] = f.B2[k]; }
-            has_global = cam != 0;
-        }
+}
+// Rodrigues of rf given the trig (th0, s0, c0) of a nearby angle th0 (the log of the FP64
+// composed rotation): cos/sin(|rf|) by a 3rd-order shift from th0 (|rf| - th0 ~ 1e-7), which
+// agrees with libm cos/sin to a few ulp; falls back to sincos if the angles are not close.
+__device__ __forceinline__ void rodrigues_near(const double r[3], double th0, double s0, double c0, Rot& o) {
+    double th;
+    {
+#pragma clang fp contract(off)
+        th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
     }
+    const double d = th - th0;
+    if (!(fabs(d) < 1e-6) || th < 1e-3) {
+        rodrigues_v2m(r, o);
+        return;
+    }
+    const double d2 = d * d;
+    const double c = c0 - s0 * d - c0 * d2 * 0.5 + s0 * d2 * d * (1.0 / 6.0);
+    const double sn = s0 + c0 * d - s0 * d2 * 0.5 - c0 * d2 * d * (1.0 / 6.0);
+    o.th = th; o.s = sn; o.c = c;
+    rodrigues_formula(r, th, sn, c, o.R);
+}
+
+
+
+// float32 composed pose -> L.T, L.R (projection) and Jl(fl32 om)
+__device__ __forceinline__ void finish_pose(const double* om, const double* T, double th, double sn, double cs,
+                                            EdgeLds& L, double* Jl) {
     // Rvectran1 / Tvectran1 -> float32 (src/mymulticalib.cpp:546-553)
     double rf[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)om[k]; L.T[k] = (double)(float)T[k]; }
     Rot rp;
-    rodrigues_v2m(rf, rp);
+    rodrigues_near(rf, th, sn, cs, rp);
 #pragma unroll
     for (int k = 0; k < 9; ++k) L.R[k] = rp.R[k];
-    double Jl[9], t9[9];
     so3_jac(rf, rp, +1.0, Jl);
-    mat3_mul(Jl, GpRR, t9);
-    store_G(L.Gp, t9, gp_tr_zero ? nullptr : GpTR, r2.R);
-    if (gg_zero) {
-        for (int k = 0; k < 36; ++k) L.Gg[k] = 0.0;
+}
+
+template <int MODEL>
+__device__ void edge_prologue(const LinArgs& a, const PhotoLds& P, const double* ctab, int e, EdgeLds& L) {
+    const int4 info = a.edge_info[e];
+    const int cam = info.x, side = info.y;
+    const double T1[3] = {P.xp[3], P.xp[4], P.xp[5]};
+    double T2[3];
+    if (MODEL == MCC_MODEL_DOUBLESIDE) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T2[k] = a.cam_rt[6 * cam + 3 + k];
+    } else if (cam == 0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T2[k] = 0.0;   // src/mymulticalib.cpp:721-725
     } else {
-        mat3_mul(Jl, GgRR, t9);
-        store_G(L.Gg, t9, gg_tr_zero ? nullptr : GgTR, GgTT);
+        const float* xc = a.x + 6 * (cam - 1);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T2[k] = xc[3 + k];
+    }
+    const double* R2 = ctab + 18 * cam;
+    const double* Jl2 = R2 + 9;
+    Motion f;
+    double th3, s3, c3;
+    compose(P.R1, P.Jr1, T1, R2, Jl2, T2, f, th3, s3, c3);
+    double Jl[9], t9[9], u9[9];
+    if (side == MCC_BACK) {
+        // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506.  R(om_front) is the FP64
+        // composed rotation itself (equal to Rodrigues(om_front) to rounding).
+        Rot rf0;
+        rf0.th = th3; rf0.s = s3; rf0.c = c3;
+        double Jlf[9];
+        so3_jac(f.om, rf0, +1.0, Jlf);
+        Motion b;
+        double th, sn, cs;
+        compose(P.Rds, P.Jrds, P.dst, f.R, Jlf, f.T, b, th, sn, cs);
+        finish_pose(b.om, b.T, th, sn, cs, L, Jl);
+        // photo: E2 * D1 = [[A2b A1, 0], [B2b A1, R2]]   (src/mymulticalib.cpp:509-512)
+        mat3_mul(b.A2, f.A1, t9);
+        mat3_mul(Jl, t9, u9);
+        mat3_mul(b.B2, f.A1, t9);
+        store_G(L.Gp, u9, t9, R2);
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {
+            // ds block: [[A1b, 0], [0, R_front]]  (src/doubleSide.cpp:398-399)
+            mat3_mul(Jl, b.A1, u9);
+            store_G(L.Gg, u9, nullptr, f.R);
+            L.has_global = 1;
+        } else {
+            // camera block as the reference chains it (src/mymulticalib.cpp:514-517), which
+            // omits dTt/dTf * dTf/dRc at :516 (hazard A12): [[A2b A2, 0], [B2b A2, I]]
+            mat3_mul(b.A2, f.A2, t9);
+            mat3_mul(Jl, t9, u9);
+            mat3_mul(b.B2, f.A2, t9);
+            store_G(L.Gg, u9, t9, nullptr);
+            L.has_global = cam != 0;
+        }
+    } else {
+        finish_pose(f.om, f.T, th3, s3, c3, L, Jl);
+        mat3_mul(Jl, f.A1, u9);
+        store_G(L.Gp, u9, nullptr, R2);
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {
+            for (int k = 0; k < 36; ++k) L.Gg[k] = 0.0;   // zero ds jacobian on the front (doubleSide.cpp:335-336)
+            L.has_global = 0;
+        } else {
+            mat3_mul(Jl, f.A2, u9);
+            store_G(L.Gg, u9, f.B2, nullptr);
+            L.has_global = cam != 0;
+        }
     }
     L.cam = cam;
     L.side = side;
     L.off = info.z;
     L.n = info.w;
-    L.has_global = has_global;
     L.edge = e;
 }
 
@@ -328,32 +372,20 @@ __device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gbl
             t[k] -= s;
         }
     }
-    const double* Lm = Lp + 36 * (size_t)p;
+    const double* Lm = Lp + kLpStride * (size_t)p;
 #pragma unroll
     for (int i = 5; i >= 0; --i) {
         double s = t[i];
 #pragma unroll
         for (int k = i + 1; k < 6; ++k) s -= Lm[k * 6 + i] * t[k];
-        t[i] = s / Lm[i * 6 + i];
+        t[i] = s * Lm[36 + i];
     }
 }
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
-#ifdef MCC_DIAG
-#define STAMP(k)                                                                                   \
-    do {                                                                                           \
-        if (threadIdx.x == 0 && a.stamps) {                                                        \
-            __builtin_amdgcn_sched_barrier(0);                                                     \
-            a.stamps[16 * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memtime();     \
-            __builtin_amdgcn_sched_barrier(0);                                                     \
-        }                                                                                          \
-    } while (0)
-#else
-#define STAMP(k) do { } while (0)
-#endif
 template <int MODEL, bool RATIONAL, bool PRISM>
-__global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
+__global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
     if (st->done) return;
     STAMP(0);
@@ -362,62 +394,117 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
     const int ne = a.photo_ptr[photo + 1] - e0;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
-    double* ph = smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double));
-    double* xp = ph;          // 6  photo params (double of the float32 state)
-    double* tk = ph + 6;      // 6
-    double* Hs = ph + 12;     // 36
-    double* gs = ph + 48;     // 6
-    double* Lm = ph + 54;     // 36 (lower)
-    double* z = ph + 90;      // 6
+    PhotoLds& P = *reinterpret_cast<PhotoLds*>(smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double)));
+    double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][18]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
-
-    // ---- phase 0: pending update of the previous step (fused back-substitution)
     const int pending = st->pending;
+
+    // ---- phase 0: stage the pending update's operands (one round trip, all threads) while
+    // wave 1 builds the camera / double-side Rodrigues tables.
     if (pending) {
-        if (tid < 6) {
-            const int k = tid;
-            double s = a.zp[6 * (size_t)photo + k];
-            for (int le = 0; le < ne; ++le) {
-                const int g = a.gblock[e0 + le];
-                if (g < 0) continue;
-                const double* Ye = a.Y + 36 * (size_t)(e0 + le);
+        for (int q = tid; q < 36 * ne; q += blockDim.x) el[q / 36].Xp[q % 36] = a.Y[36 * (size_t)e0 + q];
+        if (tid < 42) P.Lo[tid] = a.Lp[kLpStride * (size_t)photo + tid];   // L (36) + 1/L_ii (6)
+        else if (tid < 48) P.zo[tid - 42] = a.zp[6 * (size_t)photo + tid - 42];
+        for (int q = tid; q < a.global_dim; q += blockDim.x) P.dg[q] = a.dg[q];
+    }
+    if (wave == 1) {
+        if (lane < a.n_cams) {
+            const int c = lane;
+            double om2[3];
+            if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
-                for (int i = 0; i < 6; ++i) s -= Ye[i * 6 + k] * a.dg[6 * g + i];
+                for (int k = 0; k < 3; ++k) om2[k] = a.cam_rt[6 * c + k];
+            } else if (c == 0) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) om2[k] = 0.0;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) om2[k] = a.x[6 * (c - 1) + k];
             }
-            tk[k] = s;
+            Rot r2;
+            rodrigues_v2m(om2, r2);
+            double J[9];
+            so3_jac(om2, r2, +1.0, J);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { ctab[18 * c + k] = r2.R[k]; ctab[18 * c + 9 + k] = J[k]; }
+        } else if (lane == 63 && a.has_back) {
+            double dsr[3];
+            if (MODEL == MCC_MODEL_DOUBLESIDE) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { dsr[k] = a.x[k]; P.dst[k] = a.x[3 + k]; }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { dsr[k] = a.ds_rt[k]; P.dst[k] = a.ds_rt[3 + k]; }
+            }
+            Rot rd;
+            rodrigues_v2m(dsr, rd);
+            double J[9];
+            so3_jac(dsr, rd, -1.0, J);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { P.Rds[k] = rd.R[k]; P.Jrds[k] = J[k]; }
         }
-        __syncthreads();
-        if (tid == 0) {
-            const double* Lo = a.Lp + 36 * (size_t)photo;
-            double t[6];
-            for (int k = 0; k < 6; ++k) t[k] = tk[k];
-            for (int i = 5; i >= 0; --i) {
-                double s = t[i];
-                for (int k = i + 1; k < 6; ++k) s -= Lo[k * 6 + i] * t[k];
-                t[i] = s / Lo[i * 6 + i];
+    }
+    __syncthreads();
+    if (wave == 0) {
+        if (pending) {
+            // fused back-substitution of the previous step: dp = L^-T (z - sum_e Y_e^T dg_e)
+            if (lane < 6) {
+                const int k = lane;
+                double sacc = P.zo[k];
+                for (int le = 0; le < ne; ++le) {
+                    const int g = a.gblock[e0 + le];
+                    if (g < 0) continue;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) sacc -= el[le].Xp[i * 6 + k] * P.dg[6 * g + i];
+                }
+                P.tk[k] = sacc;
             }
-            const double alpha = st->alpha;
-            double g2 = 0.0, x2 = 0.0;
-            for (int k = 0; k < 6; ++k) {
-                const float G = (float)(alpha * t[k]);     // G = alpha*delta -> CV_32F (:491-496)
-                const float xn = xg[k] + G;                // x = x + G (:501)
-                xg[k] = xn;
-                xp[k] = xn;
-                g2 += (double)G * (double)G;
-                x2 += (double)xn * (double)xn;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == 0) {
+                double t[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) t[q] = P.tk[q];
+#pragma unroll
+                for (int i = 5; i >= 0; --i) {
+                    double sacc = t[i];
+#pragma unroll
+                    for (int q = i + 1; q < 6; ++q) sacc -= P.Lo[q * 6 + i] * t[q];
+                    t[i] = sacc * P.Lo[36 + i];
+                }
+                const double alpha = st->alpha;
+                double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    const float G = (float)(alpha * t[q]);     // G = alpha*delta -> CV_32F (:491-496)
+                    const float xn = xg[q] + G;                // x = x + G (:501)
+                    xg[q] = xn;
+                    P.xp[q] = xn;
+                    g2 += (double)G * (double)G;
+                    x2 += (double)xn * (double)xn;
+                }
+                a.photo_norm[2 * (size_t)photo] = g2;
+                a.photo_norm[2 * (size_t)photo + 1] = x2;
             }
-            a.photo_norm[2 * (size_t)photo] = g2;
-            a.photo_norm[2 * (size_t)photo + 1] = x2;
+        } else if (lane < 6) {
+            P.xp[lane] = xg[lane];
         }
-    } else if (tid < 6) {
-        xp[tid] = xg[tid];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
+            const double om1[3] = {P.xp[0], P.xp[1], P.xp[2]};
+            Rot r1;
+            rodrigues_v2m(om1, r1);
+            double J[9];
+            so3_jac(om1, r1, -1.0, J);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { P.R1[k] = r1.R[k]; P.Jr1[k] = J[k]; }
+        }
     }
     __syncthreads();
     STAMP(1);
 
     // ---- phase A: edge prologues, one lane per edge
-    for (int le = tid; le < ne; le += blockDim.x) edge_prologue<MODEL>(a, xp, e0 + le, el[le]);
+    for (int le = tid; le < ne; le += blockDim.x) edge_prologue<MODEL>(a, P, ctab, e0 + le, el[le]);
     __syncthreads();
     STAMP(2);
 
@@ -526,37 +613,60 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
 
     // ---- phase D: photo block: Hpp = sum_e, Cholesky, z = L^-1 gp, Y_e = Hgp_e L^-T
     STAMP(5);
+    double* Hs = P.Hs;
+    double* gs = P.gs;
+    double* Lm = P.Lm;
+    double* z = P.z;
     if (tid < 42) {
-        double s = 0.0;
-        for (int le = 0; le < ne; ++le) s += tid < 36 ? el[le].Hpp[tid] : el[le].gp[tid - 36];
-        if (tid < 36) Hs[tid] = s; else gs[tid - 36] = s;
+        double sacc = 0.0;
+        for (int le = 0; le < ne; ++le) sacc += tid < 36 ? el[le].Hpp[tid] : el[le].gp[tid - 36];
+        if (tid < 36) Hs[tid] = sacc; else gs[tid - 36] = sacc;
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0) {   // register-resident 6x6 Cholesky (packed lower, in place) + forward substitution
+        double Lr[21], il[6], zz[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) Lr[i * (i + 1) / 2 + j] = Hs[i * 6 + j];
         int ok = 1;
+#pragma unroll
         for (int j = 0; j < 6; ++j) {
-            double s = Hs[j * 6 + j];
-            for (int k = 0; k < j; ++k) s -= Lm[j * 6 + k] * Lm[j * 6 + k];
-            if (!(s > 0.0)) { ok = 0; s = 1.0; }
-            const double l = sqrt(s), il = 1.0 / l;
-            Lm[j * 6 + j] = l;
+            double sacc = Lr[j * (j + 1) / 2 + j];
+#pragma unroll
+            for (int q = 0; q < j; ++q) sacc -= Lr[j * (j + 1) / 2 + q] * Lr[j * (j + 1) / 2 + q];
+            if (!(sacc > 0.0)) { ok = 0; sacc = 1.0; }
+            const double l = sqrt(sacc);
+            il[j] = 1.0 / l;
+            Lr[j * (j + 1) / 2 + j] = l;
+#pragma unroll
             for (int i = j + 1; i < 6; ++i) {
-                double t = Hs[i * 6 + j];
-                for (int k = 0; k < j; ++k) t -= Lm[i * 6 + k] * Lm[j * 6 + k];
-                Lm[i * 6 + j] = t * il;
+                double t = Lr[i * (i + 1) / 2 + j];
+#pragma unroll
+                for (int q = 0; q < j; ++q) t -= Lr[i * (i + 1) / 2 + q] * Lr[j * (j + 1) / 2 + q];
+                Lr[i * (i + 1) / 2 + j] = t * il[j];
             }
-            for (int i = 0; i < j; ++i) Lm[i * 6 + j] = 0.0;
         }
+#pragma unroll
         for (int i = 0; i < 6; ++i) {
-            double s = gs[i];
-            for (int k = 0; k < i; ++k) s -= Lm[i * 6 + k] * z[k];
-            z[i] = s / Lm[i * 6 + i];
+            double sacc = gs[i];
+#pragma unroll
+            for (int q = 0; q < i; ++q) sacc -= Lr[i * (i + 1) / 2 + q] * zz[q];
+            zz[i] = sacc * il[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            z[i] = zz[i];
+            P.il[i] = il[i];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) Lm[i * 6 + j] = j <= i ? Lr[i * (i + 1) / 2 + j] : 0.0;
         }
         if (!ok) atomicOr(&st->error, 1);
     }
     __syncthreads();
     STAMP(6);
-    if (tid < 36) a.Lp[36 * (size_t)photo + tid] = Lm[tid];
+    if (tid < 36) a.Lp[kLpStride * (size_t)photo + tid] = Lm[tid];
+    else if (tid >= 48 && tid < 54) a.Lp[kLpStride * (size_t)photo + 36 + tid - 48] = P.il[tid - 48];
     else if (tid < 42) a.zp[6 * (size_t)photo + tid - 36] = z[tid - 36];
     else if (tid < 48) a.gp_tot[6 * (size_t)photo + tid - 42] = gs[tid - 42];
     for (int t = tid; t < 6 * ne; t += blockDim.x) {
@@ -568,7 +678,7 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
             for (int j = 0; j < 6; ++j) {
                 double s = L.Hgp[i * 6 + j];
                 for (int k = 0; k < j; ++k) s -= Lm[j * 6 + k] * y[k];
-                y[j] = s / Lm[j * 6 + j];
+                y[j] = s * P.il[j];
             }
         } else {
             for (int j = 0; j < 6; ++j) y[j] = 0.0;
@@ -588,13 +698,63 @@ __global__ __launch_bounds__(256) void k_linearize(LinArgs a) {
 }
 
 // ---------------------------------------------------------------- global solve (one workgroup)
-// Stop test (src/multicalib.cpp:475-477), Cholesky of S (m <= 128, Crout, rows spread over the
-// 256 threads, one barrier per column), triangular solves (one wavefront, shuffle dot
-// products), global-block delta and float32 update.  S (m x m, overwritten by L in its lower
-// triangle) and r (m) are in LDS.
+// Stop test (src/multicalib.cpp:475-477), elimination of the reduced camera system (m <= 128),
+// global-block delta and float32 update.  S (m x m) and r (m) are in LDS and are overwritten.
 __device__ __forceinline__ double sub_sum(double v, int tpr) {
     for (int o = 1; o < tpr; o <<= 1) v += __shfl_xor(v, o);
     return v;
+}
+
+// Gauss-Jordan of [S | r] (m x (m+1), m <= 30) by one wavefront with the matrix in registers: lane j
+// owns column j (lane m owns r), pivot columns are broadcast with v_readlane (uniform lane
+// index), every loop is unrolled at compile time (MM >= m).  No LDS traffic, no barriers.
+// Writes delta_i = r_i / S_ii into r[].
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+template <int MM>
+__device__ __forceinline__ void gj_wave(const double* S, double* r, int m, int lane, int* err) {
+    // every load address is in range for every lane (nothing speculated past the LDS arrays):
+    // lanes >= m read column 0 / r[0] and are masked to 0 afterwards
+    const int lc = lane < m ? lane : 0;
+    double col[MM];
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {
+        const int ii = i < m ? i : 0;
+        const double vs = S[ii * m + lc];
+        const double vr = r[ii];
+        col[i] = (i < m && lane <= m) ? (lane < m ? vs : vr) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < MM; ++k) {
+        if (k >= m) break;
+        const double piv = readlane_f64(col[k], k);
+        if (!(piv > 0.0) && lane == 0) atomicOr(err, 2);
+        const double f = col[k] / (piv > 0.0 ? piv : 1.0);
+#pragma unroll
+        for (int i = 0; i < MM; ++i)
+            if (i != k) col[i] -= readlane_f64(col[i], k) * f;
+    }
+    // lane m holds the eliminated r; divide by the diagonal (lane i's col[i])
+#pragma unroll
+    for (int i = 0; i < MM; ++i) {
+        if (i >= m) break;
+        const double dii = readlane_f64(col[i], i);
+        if (lane == m) r[i] = col[i] / dii;
+    }
+}
+
+__device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err) {
+    switch (m) {
+#define GJ(M) case M: gj_wave<M>(S, r, m, lane, err); break;
+        GJ(6) GJ(12) GJ(18) GJ(24) GJ(30)
+#undef GJ
+        default: break;
+    }
 }
 
 __device__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
@@ -619,54 +779,39 @@ __device__ void solve_global(const SolveCtx& a, double* S, double* r, double nor
     }
     __syncthreads();
     if (stop) return;
-    // ---- Crout: L[i][j] = (S[i][j] - sum_{k<j} L[i][k] L[j][k]) / L[j][j]
-    const int tpr = m <= 32 ? 8 : (m <= 64 ? 4 : 2);   // threads per row (same wavefront)
-    const int row = tid / tpr, sub = tid % tpr;
-    for (int j = 0; j < m; ++j) {
-        double dj = 0.0, di = 0.0;
-        const bool act = row < m && row >= j;
-        if (act) {
-            for (int k = sub; k < j; k += tpr) {
-                const double ljk = S[j * m + k];
-                dj += ljk * ljk;
-                di += S[row * m + k] * ljk;
+    STAMPP(a.stamps, 8, 4);
+    if (m <= 30) {
+        if (tid < 64) gj_dispatch(S, r, m, tid, &st->error);
+        __syncthreads();
+    } else {
+        // ---- Gauss-Jordan elimination of [S | r] without row scaling (S is SPD: no pivoting).
+        // Step k updates rows i != k, columns j > k and r from the (unchanged) pivot row/column, so
+        // nothing read in step k is written in step k: one barrier per step, no cross-lane
+        // reductions.  Afterwards delta_i = r_i / S_ii.
+        const int W = m + 1;   // columns k+1..m-1 plus r
+        for (int kk = 0; kk < m; ++kk) {
+            const double piv = S[kk * m + kk];
+            if (!(piv > 0.0) && tid == 0) atomicOr(&st->error, 2);
+            const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
+            const int ncol = m - kk;   // j in kk+1..m-1 (ncol-1 of them) + r
+            for (int i = tid >> 4; i < m; i += 16) {
+                if (i == kk) continue;
+                const double f = S[i * m + kk] * ip;
+                for (int c = tid & 15; c < ncol; c += 16) {
+                    if (c == ncol - 1) r[i] -= f * r[kk];
+                    else S[i * m + kk + 1 + c] -= f * S[kk * m + kk + 1 + c];
+                }
             }
+            __syncthreads();
         }
-        dj = sub_sum(dj, tpr);
-        di = sub_sum(di, tpr);
-        if (act && sub == 0) {
-            double d = S[j * m + j] - dj;
-            if (!(d > 0.0)) {
-                if (row == j) atomicOr(&st->error, 2);
-                d = 1.0;
-            }
-            const double l = sqrt(d);
-            if (row == j) S[j * m + j] = l;
-            else S[row * m + j] = (S[row * m + j] - di) / l;
-        }
+        (void)W;
+
+        for (int i = tid; i < m; i += blockDim.x) r[i] = r[i] / S[i * m + i];
         __syncthreads();
     }
-    // ---- L y = r, L^T x = y (one wavefront; lanes split the dot products)
+    STAMPP(a.stamps, 8, 5);
     if (tid < 64) {
         const int lane = tid;
-        for (int j = 0; j < m; ++j) {
-            double s = 0.0;
-            for (int k = lane; k < j; k += 64) s += S[j * m + k] * r[k];
-            s = wave_sum(s);
-            const double yj = (r[j] - s) / S[j * m + j];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane == 0) r[j] = yj;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
-        for (int j = m - 1; j >= 0; --j) {
-            double s = 0.0;
-            for (int k = j + 1 + lane; k < m; k += 64) s += S[k * m + j] * r[k];
-            s = wave_sum(s);
-            const double xj = (r[j] - s) / S[j * m + j];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane == 0) r[j] = xj;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        }
         // global block: delta, update, norm partials (identical on every rank)
         const double alpha = st->alpha;
         double g2 = 0.0, x2 = 0.0;
@@ -682,6 +827,7 @@ __device__ void solve_global(const SolveCtx& a, double* S, double* r, double nor
                 x2 += (double)xn * (double)xn;
             }
         }
+        STAMPP(a.stamps, 8, 6);
         g2 = wave_sum(g2);
         x2 = wave_sum(x2);
         if (lane == 0 && a.do_update) {
@@ -700,9 +846,11 @@ __device__ void solve_global(const SolveCtx& a, double* S, double* r, double nor
 // system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2] in fixed order, and with
 // fuse_solve (single GPU) solves it in place.
 constexpr int kSub = 5;
+constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
 __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
+    STAMPP(a.stamps, 8, 0);
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
     __shared__ double part[kSub][48];
@@ -713,6 +861,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         const int q = tid % 48, sub = tid / 48;
         double s = 0.0;
         if (sub < kSub) {
+#pragma unroll 4
             for (int p = it.y + sub; p < it.z; p += kSub) {
                 const int4 pr = a.pairs[p];   // {e1, e2, photo, self}
                 const double* Y1 = a.Y + 36 * (size_t)pr.x;
@@ -760,6 +909,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             __syncthreads();
         }
     }
+    STAMPP(a.stamps, 8, 1);
     // ---- publish the partial, take a ticket (agent-scope release/acquire, cdna guide G16)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -777,48 +927,65 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    STAMPP(a.stamps, 8, 2);
     // ---- assemble (fixed order): S full into LDS, packed to global
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     double* S = sm;          // m*m
     double* r = sm + m * m;  // m
     __shared__ double norms[2];
-    for (int t = tid; t < m * m + 2 * m + 2; t += blockDim.x) {
+    for (int t = tid; t < ntri + 2 * m + 2; t += blockDim.x) {
         double v = 0.0;
-        if (t < m * m) {
-            const int i = t / m, j = t % m;
-            if (j < i) continue;
-            const int b1 = i / 6, b2 = j / 6, ii = i % 6, jj = j % 6;
-            const int blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
-            const int k0 = a.block_items[blk], k1 = a.block_items[blk + 1];
-            const double* src = a.item_out + ii * 6 + jj;
-#pragma unroll 8
-            for (int k = k0; k < k1; ++k) v += src[48 * (size_t)k];
-            S[i * m + j] = v;
-            S[j * m + i] = v;
-            a.packed[i * m - i * (i - 1) / 2 + (j - i)] = v;
-        } else if (t < m * m + 2 * m) {
-            const int u = t - m * m, g = u % m, w = u / m, b = g / 6;
-            const int blk = b * nb - b * (b - 1) / 2;
-            const int k0 = a.block_items[blk], k1 = a.block_items[blk + 1];
-            const double* src = a.item_out + 36 + 6 * w + g % 6;
-#pragma unroll 8
-            for (int k = k0; k < k1; ++k) v += src[48 * (size_t)k];
-            if (w == 0) r[g] = v;
-            a.packed[ntri + u] = v;
+        if (t < ntri + 2 * m) {
+            int i, j, w = 0, blk;
+            const double* src;
+            if (t < ntri) {
+                // packed upper index -> (i, j): row i holds m - i entries
+                i = (int)((2.0 * m + 1.0 - sqrt((2.0 * m + 1.0) * (2.0 * m + 1.0) - 8.0 * t)) * 0.5);
+                while (i > 0 && i * m - i * (i - 1) / 2 > t) --i;
+                while ((i + 1) * m - (i + 1) * i / 2 <= t) ++i;
+                j = i + (t - (i * m - i * (i - 1) / 2));
+                const int b1 = i / 6, b2 = j / 6;
+                blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
+                src = a.item_out + (i % 6) * 6 + (j % 6);
+            } else {
+                const int u = t - ntri;
+                i = u % m; j = i; w = u / m;
+                const int b = i / 6;
+                blk = b * nb - b * (b - 1) / 2;
+                src = a.item_out + 36 + 6 * w + i % 6;
+            }
+            const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
+            // unconditional loads (item_out is padded by kMaxItemsPerBlock zeroed items), masked
+            // adds: no branch around the loads (cdna guide section 5, item 4(c))
+            double part[kMaxItemsPerBlock];
+#pragma unroll
+            for (int q = 0; q < kMaxItemsPerBlock; ++q) part[q] = src[48 * (size_t)(k0 + q)];
+#pragma unroll
+            for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? part[q] : 0.0;
+            if (t < ntri) {
+                S[i * m + j] = v;
+                S[j * m + i] = v;
+            } else if (w == 0) {
+                r[i] = v;
+            }
         } else {
-            const int w = t - m * m - 2 * m;   // 0: normG2, 1: normX2 of the last update
+            const int w = t - ntri - 2 * m;   // 0: normG2, 1: normX2 of the last update
             if (st->iter > 0) {
                 for (int k = a.n_items; k < (int)gridDim.x; ++k) v += a.item_out[48 * (size_t)k + w];
                 if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
             }
             norms[w] = v;
-            a.packed[ntri + 2 * m + w] = v;
         }
+        a.packed[t] = v;
     }
     if (!a.fuse_solve) return;
     __syncthreads();
-    solve_global(a.solve, S, r, norms[0], norms[1]);
+    STAMPP(a.stamps, 8, 3);
+    SolveCtx sc = a.solve;
+    sc.stamps = a.stamps;
+    solve_global(sc, S, r, norms[0], norms[1]);
+    STAMPP(a.stamps, 8, 7);
 }
 
 // ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)
@@ -1003,14 +1170,14 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     return hipGetLastError();
 }
 
-size_t mcc_lin_shmem(int max_edges_per_photo) {
-    return (size_t)max_edges_per_photo * sizeof(EdgeLds) + kPhotoScratch * sizeof(double);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams) {
+    return (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) + 18 * sizeof(double) * (size_t)n_cams;
 }
 
 size_t mcc_solve_shmem(int m) { return (size_t)(m * m + m) * sizeof(double); }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp);
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
         case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
@@ -1018,9 +1185,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int m) {
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m) {
     hipError_t err = hipSuccess;
-    const size_t shmem = mcc_lin_shmem(max_epp);
+    const size_t shmem = mcc_lin_shmem(max_epp, n_cams);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
         for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),

@@ -68,3 +68,20 @@ def test_optimize(case):
     assert it == it_ref, (name, it, it_ref)
     assert abs(m - m_ref) <= 1e-6, (name, m, m_ref)
     assert np.abs(x - x_ref).max() <= 1e-4 * np.abs(x_ref).max(), name
+
+
+def test_step_flush(case):
+    """mcc_step (pending photo updates fused into the next linearisation) then get_params
+    equals the oracle's optimizeExtrinsics with TermCriteria COUNT = n."""
+    name, p, o, g = case
+    n = 4
+    x_ref, _, it_ref, _ = o.optimize(p.x0, crit_type=1, max_count=n)
+    g.set_params(p.x0)
+    g.step(n)
+    x = g.get_params()
+    assert it_ref == n
+    assert np.abs(x - x_ref).max() <= 1e-4 * np.abs(x_ref).max(), name
+    # linearisation after a flushed state starts from the same x
+    d_ref, _ = o.linearize_solve(x_ref, "schur")
+    d, _ = g.compute_jacobian_extrinsic(x)
+    assert np.abs(d - d_ref).max() <= 1e-6 * np.abs(d_ref).max(), name

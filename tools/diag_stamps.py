@@ -27,7 +27,11 @@ def main():
     ba.stamps()          # arm
     ba.step(3)
     ba.synchronize()
-    s = ba.stamps().astype(np.float64)
+    raw = ba.stamps().reshape(-1)
+    nv = max(p.n_photos, 1)
+    lin = raw[:16 * nv].reshape(nv, 16).astype(np.float64)
+    sch = raw[16 * nv:].reshape(-1, 8).astype(np.float64)
+    s = lin
     t0 = s[:, 0]
     ok = t0 > 0
     s = s[ok]
@@ -41,6 +45,17 @@ def main():
     print(f"  {'total':16s} median {np.median(tot):9.0f}  p90 {np.percentile(tot, 90):9.0f}")
     span = s[:, 7].max() - s[:, 0].min()
     print(f"  kernel span (first start -> last end): {span:.0f} ticks; start spread {s[:, 0].max() - s[:, 0].min():.0f}")
+    ok = sch[:, 0] > 0
+    it = sch[ok]
+    print(f"k_schur: {ok.sum()} workgroups; item compute median {np.median(it[:, 1] - it[:, 0]):.0f}, "
+          f"ticket median {np.median(it[:, 2] - it[:, 1]):.0f} (non-last rows have 0 in slot 2)")
+    last = sch[sch[:, 3] > 0]
+    if len(last):
+        L = last[0]
+        names = ["start", "items", "acquire", "assembly", "stoptest", "crout", "trisolve", "end"]
+        print("  last arriver: " + ", ".join(f"{names[k]}->{names[k+1]} {L[k+1]-L[k]:.0f}" for k in range(7)))
+        print(f"  kernel span {sch[ok, 0].min():.0f} -> {L[7]:.0f}: {L[7] - sch[ok, 0].min():.0f} ticks; "
+              f"last item start {sch[ok, 0].max() - sch[ok, 0].min():.0f} after the first")
 
 
 if __name__ == "__main__":
