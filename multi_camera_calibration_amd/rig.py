@@ -441,3 +441,26 @@ def subset_photos(p: Problem, photos) -> Problem:
                    ds_pose=p.ds_pose, cam_pose=p.cam_pose, x0=p.x0[cols].copy(),
                    x_true=p.x_true[cols].copy(), timestamps=p.timestamps[photos],
                    image_size=p.image_size, name=p.name + "[subset]")
+
+
+# ----------------------------------------------------------------------------- (de)serialisation
+_ARRAY_FIELDS = ("edge_cam", "edge_photo", "edge_side", "edge_off", "edge_n", "obj", "img", "K", "D",
+                 "xi", "ds_pose", "cam_pose", "x0", "x_true", "timestamps")
+
+
+def problem_to_arrays(p: Problem, prefix: str = "") -> dict:
+    """Flat dict of numpy arrays (npz-ready, no pickles) holding every input of a Problem."""
+    out = {prefix + "meta": np.array([p.model, p.n_cams, p.n_photos, p.image_size[0], p.image_size[1]],
+                                     np.int64)}
+    for f in _ARRAY_FIELDS:
+        v = getattr(p, f)
+        if v is not None:
+            out[prefix + f] = np.asarray(v)
+    return out
+
+
+def problem_from_arrays(a, prefix: str = "", name: str = "") -> Problem:
+    meta = [int(v) for v in a[prefix + "meta"]]
+    kw = {f: (np.array(a[prefix + f]) if (prefix + f) in a else None) for f in _ARRAY_FIELDS}
+    return Problem(model=meta[0], n_cams=meta[1], n_photos=meta[2], image_size=(meta[3], meta[4]),
+                   name=name, **kw)

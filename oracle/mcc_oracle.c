@@ -910,6 +910,33 @@ out:
     return rc;
 }
 
+/* Photo back-substitution for a given global step dg (m): dp_v = Hpp^-1 (gp - sum_e Hgp_e^T dg_e)
+ * for photos [lo, hi), written to dphoto[6 * (v - lo)] (the rank-local half of a sharded step). */
+int ora_photo_backsub(const ora_problem *p, const float *x, int lo, int hi, const double *dg,
+                      double *dphoto)
+{
+    sparse_ws w;
+    int rc = build_ws(p, x, &w);
+    for (int v = lo; v < hi && !rc; ++v) {
+        double L[36] = {0}, gp[6] = {0}, t[6] = {0};
+        for (int q = w.ptr[v]; q < w.ptr[v + 1]; ++q) {
+            const edge_blk *b = &w.blk[w.idx[q]];
+            for (int k = 0; k < 36; ++k) L[k] += b->Hpp[k];
+            for (int k = 0; k < 6; ++k) gp[k] += b->gp[k];
+            int g = gblock(p, w.idx[q]);
+            if (g < 0) continue;
+            for (int k = 0; k < 6; ++k)
+                for (int i = 0; i < 6; ++i) t[k] += b->Hgp[i * 6 + k] * dg[g * 6 + i];
+        }
+        if (cholesky(L, 6)) { rc = -5; break; }
+        chol_solve(L, 6, gp);
+        chol_solve(L, 6, t);
+        for (int k = 0; k < 6; ++k) dphoto[6 * (v - lo) + k] = gp[k] - t[k];
+    }
+    free_ws(&w);
+    return rc;
+}
+
 int ora_linearize_solve(const ora_problem *p, const float *x, int solver, double *delta,
                         double *jte)
 {

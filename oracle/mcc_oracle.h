@@ -108,6 +108,11 @@ int ora_global_dim(const ora_problem *p);
 int ora_schur_partial(const ora_problem *p, const float *x, int photo_lo, int photo_hi,
                       double *S, double *r);
 
+/* Back-substitution of the photo blocks [lo, hi) for a given global step dg[m]:
+ * dphoto[6 * (hi - lo)] (the rank-local half of a photo-sharded step). */
+int ora_photo_backsub(const ora_problem *p, const float *x, int lo, int hi, const double *dg,
+                      double *dphoto);
+
 /* The optimizeExtrinsics loop.  crit_type: 1 COUNT, 2 EPS, 3 COUNT+EPS.  Returns the
  * computeProjectError mean (or a negative value on failure). */
 double ora_optimize(const ora_problem *p, int crit_type, int max_count, double eps, int solver,

@@ -118,6 +118,15 @@ class Oracle:
             raise RuntimeError(f"ora_schur_partial failed: {rc}")
         return S, r
 
+    def photo_backsub(self, x, lo, hi, dg):
+        x = np.ascontiguousarray(x, np.float32)
+        dg = np.ascontiguousarray(dg, np.float64)
+        out = np.zeros(6 * (hi - lo))
+        rc = lib().ora_photo_backsub(ctypes.byref(self.s), _p(x, _f32p), lo, hi, _p(dg, _f64p), _p(out, _f64p))
+        if rc:
+            raise RuntimeError(f"ora_photo_backsub failed: {rc}")
+        return out
+
     def optimize(self, x, crit_type=3, max_count=200, eps=1e-7, solver="schur"):
         x = np.array(x, np.float32, copy=True)
         it = ctypes.c_int(0); ch = ctypes.c_double(0)
