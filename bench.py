@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="config2")
     ap.add_argument("--views", type=int, default=None, help="views per rank (default: the config's)")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
