@@ -109,6 +109,9 @@ struct mcc_problem {
     bool rational = false, prism = false;
     int has_back = 0;
     int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
+    // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
+    static constexpr int kFusedMaxM = 30;
+    int fused = 0, group_size = 1, n_groups = 1;
     hipStream_t stream = nullptr;
 
     // host-side maps
@@ -119,8 +122,8 @@ struct mcc_problem {
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
-    DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha;
-    DevBuf<int> photo_ptr, edge_gblock, block_items, edge_photo, counter;
+    DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum;
+    DevBuf<int> photo_ptr, edge_gblock, block_items, edge_photo, counter, cnt;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
@@ -170,12 +173,32 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.dg = p->dg.p;
     la.photo_norm = p->photo_norm.p;
     la.stamps = p->stamps.p;
+    // any communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
+    // split path: the packed system is summed by RCCL and solved by k_solve
+    const bool multi = p->comm != nullptr;
+    la.fused = p->fused;
+    la.group_size = p->group_size; la.n_groups = p->n_groups;
+    la.rank = p->rank; la.fuse_solve = multi ? 0 : 1;
+    la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p;
+    la.solve = solve_ctx(p, do_update);
+    la.solve.stamps = nullptr;
     if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
+    if (p->fused) {
+        if (multi) {
+            ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
+                                           p->comm, p->stream);
+            if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            SolveArgs so{solve_ctx(p, do_update), p->packed.p};
+            HIPCHK(mcc_launch_solve(so, p->stream));
+        }
+        if (tim) {
+            HIPCHK(hipEventRecord(p->ev_step[p->ev_used + 1], p->stream));
+            p->ev_used += 2;
+        }
+        return MCC_OK;
+    }
 
-    // any communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
-    // split path: k_schur assembles, RCCL sums the packed system, k_solve solves it
-    const bool multi = p->comm != nullptr;
     SchurArgs sa{};
     sa.state = p->state.p;
     sa.items = p->items.p; sa.pairs = p->pairs.p;
@@ -419,6 +442,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->n_pairs = (int)pairs.size();
     p->n_norm_chunks = (V + 255) / 256;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
+    // small camera blocks: one kernel per Gauss-Newton step (MCC_FUSED=0 forces the k_schur path)
+    p->fused = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
+    if (const char* f = std::getenv("MCC_FUSED")) p->fused = p->fused && std::atoi(f) != 0;
+    p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
+    p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;
 
     // ---- fixed transforms
     std::vector<float> cam_rt(6 * C, 0.f);
@@ -479,6 +507,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->packed.alloc(p->packed_len));
     HIPC(p->dg.alloc(p->m)); HIPC(p->delta.alloc(p->P));
     HIPC(p->photo_norm.alloc(2 * (size_t)V));
+    if (p->fused) {
+        HIPC(p->contrib.alloc((size_t)p->packed_len * std::max(V, 1)));
+        HIPC(p->gsum.alloc((size_t)p->packed_len * p->n_groups));
+        HIPC(p->cnt.alloc(p->n_groups + 1));
+        HIPC(hipMemset(p->cnt.p, 0, sizeof(int) * (p->n_groups + 1)));
+    }
     HIPC(hipMemset(p->photo_norm.p, 0, sizeof(double) * 2 * std::max(V, 1)));
     HIPC(p->edge_sum.alloc(E));
     HIPC(p->state.alloc(1));
@@ -487,8 +521,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
-    if (mcc_lin_shmem(p->max_epp, C) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m));
+    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -507,6 +541,7 @@ void mcc_destroy(mcc_problem* p) {
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
+    p->contrib.release(); p->gsum.release(); p->cnt.release();
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Lp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();

@@ -21,6 +21,16 @@ struct State {
     int pending;      // a solved photo update waits to be applied by the next k_linearize
 };
 
+struct SolveCtx {
+    State* state;
+    const double* alpha; int n_alpha;
+    float* x;
+    double* dg;       // [m]
+    double* delta;    // [P]
+    int m, do_update;
+    long long* stamps;   // MCC_DIAG: solve phase stamps (set by k_schur's last arriver)
+};
+
 struct LinArgs {
     State* state;
     const int* photo_ptr;     // [V+1] photo-major edge ranges
@@ -45,16 +55,16 @@ struct LinArgs {
     const double* dg;        // [m] global-block delta of the previous solve
     double* photo_norm;      // [2V] ||G||^2, ||x||^2 partials of the applied update
     long long* stamps;       // MCC_DIAG builds: [16V] s_memtime per phase
-};
-
-struct SolveCtx {
-    State* state;
-    const double* alpha; int n_alpha;
-    float* x;
-    double* dg;       // [m]
-    double* delta;    // [P]
-    int m, do_update;
-    long long* stamps;   // MCC_DIAG: solve phase stamps (set by k_schur's last arriver)
+    // fused single-kernel step (m <= 30): every photo writes its packed contribution
+    // [S upper | r | jte_g | normG2 | normX2], a fixed-order two-level last-arriver reduction sums
+    // them (groups of group_size consecutive photos, then the groups), and the final arriver
+    // solves (fuse_solve) or leaves the packed system for the all-reduce + k_solve
+    int fused, group_size, n_groups, rank, fuse_solve;
+    double* contrib;         // [V * Lc]
+    double* gsum;            // [n_groups * Lc]
+    int* cnt;                // [n_groups + 1] tickets, zero between launches
+    double* packed;          // [Lc]
+    SolveCtx solve;
 };
 
 struct SchurArgs {
@@ -104,9 +114,9 @@ struct ErrArgs {
 }  // namespace mcc
 
 // launch wrappers (mcc_kernels.hip)
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m);
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);

@@ -37,6 +37,16 @@ namespace mcc {
 #define STAMPP(ptr, stride, k) do { } while (0)
 #endif
 #define STAMP(k) STAMPP(a.stamps, 16, k)
+// chip-wide 100 MHz clock (s_memtime is per XCD): cross-workgroup timelines
+#ifdef MCC_DIAG
+#define RSTAMP(k)                                                                                  \
+    do {                                                                                           \
+        if (threadIdx.x == 0 && a.stamps)                                                          \
+            a.stamps[16 * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define RSTAMP(k) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------- wave reduction
 // Reduce-scatter butterfly of 32 per-lane doubles across the 64 lanes: 32 shuffles of 64-bit
@@ -115,6 +125,8 @@ struct PhotoLds {
     double Lo[42], zo[6], tk[6];     // pending-update staging (L, 1/L_ii, z)
     double Hs[36], gs[6], Lm[36], z[6], il[6];
     double dg[128];      // global-block delta of the previous solve
+    double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
+    int eg[64];          // global block of each edge of the photo or -1 (fused step)
     // followed by the camera table: [C][18] = {R (9), Jl (9)}
 };
 static_assert(sizeof(PhotoLds) % 16 == 0, "PhotoLds alignment");
@@ -382,6 +394,80 @@ __device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gbl
     }
 }
 
+// ---------------------------------------------------------------- cross-workgroup hand-off
+// Publish this workgroup's global stores and take a ticket; returns true (uniformly) in the
+// last of `expected` arrivals, which then sees every other arrival's stores.  Agent-scope
+// release/acquire as in /opt/skills/guides/cdna_hip_programming.md section 6 (G16); the last
+// arriver resets the counter for the next launch.
+__device__ __forceinline__ bool arrive_last(int* counter, int expected) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t == expected - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    return last;
+}
+
+// Write-through (sc1) hand-off without release/acquire fences, MI355X_MICROARCH.md section
+// "visibility", Valid forms table row 1: every handed-off double is stored with an 8-B agent-scope
+// relaxed atomic store (global_store sc1), every storing wave drains vmcnt(0) before the
+// workgroup barrier, ONE lane adds to the counter, the workgroup whose add came last loads every
+// handed-off double with sc1 loads after a barrier.  (A release fence here writes back the XCD
+// L2's freshly dirtied lines of the whole linearisation: ~6 us per workgroup.)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ bool arrive_last_sc1(int* counter, int expected) {
+    __shared__ int last_sc1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add((gi32*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sc1 = (t == expected - 1);
+        if (last_sc1) __hip_atomic_store((gi32*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    return last_sc1;
+}
+
+// packed upper-triangle index t -> (i, j), row i holding m - i entries
+__device__ __forceinline__ void packed_ij(int t, int m, int& i, int& j) {
+    int rem = t, row = 0;
+    while (rem >= m - row) { rem -= m - row; ++row; }
+    i = row;
+    j = row + rem;
+}
+
+// sum_{q < n} p[q * stride] in q order with sc1 loads issued 8 at a time (in flight together)
+__device__ __forceinline__ double sum_sc1(const double* p, int n, size_t stride) {
+    double v = 0.0;
+    for (int q0 = 0; q0 < n; q0 += 8) {
+        double b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = ld_sc1(p + (size_t)min(q0 + u, n - 1) * stride);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += q0 + u < n ? b[u] : 0.0;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2);
+
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
 template <int MODEL, bool RATIONAL, bool PRISM>
@@ -389,6 +475,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
     if (st->done) return;
     STAMP(0);
+    RSTAMP(14);
     const int photo = blockIdx.x;
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
@@ -485,9 +572,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 }
                 a.photo_norm[2 * (size_t)photo] = g2;
                 a.photo_norm[2 * (size_t)photo + 1] = x2;
+                P.nrm[0] = g2;
+                P.nrm[1] = x2;
             }
         } else if (lane < 6) {
             P.xp[lane] = xg[lane];
+        } else if (lane < 8) {
+            P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // written by a k_backsub flush
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
@@ -671,7 +762,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     else if (tid < 48) a.gp_tot[6 * (size_t)photo + tid - 42] = gs[tid - 42];
     for (int t = tid; t < 6 * ne; t += blockDim.x) {
         const int le = t / 6, i = t % 6;
-        const EdgeLds& L = el[le];
+        EdgeLds& L = el[le];
         const int e = e0 + le;
         double y[6];
         if (L.has_global) {
@@ -684,17 +775,122 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             for (int j = 0; j < 6; ++j) y[j] = 0.0;
         }
         double* Yo = a.Y + 36 * (size_t)e + 6 * i;
-        double* Ho = a.Hgg + 36 * (size_t)e + 6 * i;
-        for (int j = 0; j < 6; ++j) {
-            Yo[j] = y[j];
-            Ho[j] = L.has_global ? L.Hgg[i * 6 + j] : 0.0;
+        if (a.fused) {
+            // Xg (A' Gg scratch) is dead: it holds row i of Y_e for the contribution below
+            for (int j = 0; j < 6; ++j) { Yo[j] = y[j]; L.Xg[i * 6 + j] = y[j]; }
+        } else {
+            double* Ho = a.Hgg + 36 * (size_t)e + 6 * i;
+            for (int j = 0; j < 6; ++j) {
+                Yo[j] = y[j];
+                Ho[j] = L.has_global ? L.Hgg[i * 6 + j] : 0.0;
+            }
+            a.gg[6 * (size_t)e + i] = L.has_global ? L.gg[i] : 0.0;
         }
-        a.gg[6 * (size_t)e + i] = L.has_global ? L.gg[i] : 0.0;
     }
+    if (!a.fused) {
 #ifdef MCC_DIAG
+        __syncthreads();
+        STAMP(7);
+        RSTAMP(15);
+#endif
+        return;
+    }
+
+    if (tid < ne) {
+        const EdgeLds& L = el[tid];
+        P.eg[tid] = L.has_global ? (MODEL == MCC_MODEL_DOUBLESIDE ? 0 : L.cam - 1) : -1;
+    }
+    // ---- phase E (fused step, m <= 30): this photo's packed contribution
+    //   S[i][j] (i <= j) = sum_{a: g_a = i/6} sum_{b: g_b = j/6} ([a == b] Hgg_a - Y_a Y_b^T)[i%6][j%6]
+    //   r[i] = sum_{a: g_a = i/6} (gg_a - Y_a z)[i%6],  jte_g[i] = sum gg_a[i%6],  norms of the update
+    // (k_schur's pair sums, src/multicalib.cpp:565-579 normal equations reduced onto the cameras)
     __syncthreads();
     STAMP(7);
-#endif
+    const int m = a.global_dim, ntri = m * (m + 1) / 2, Lc = ntri + 2 * m + 2;
+    double* cv = a.contrib + (size_t)photo * Lc;
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        if (t < ntri) {
+            int i, j;
+            packed_ij(t, m, i, j);
+            const int bi = i / 6, bj = j / 6, ii = i % 6, jj = j % 6;
+            for (int ea = 0; ea < ne; ++ea) {
+                if (P.eg[ea] != bi) continue;
+                const EdgeLds& La = el[ea];
+                for (int eb = 0; eb < ne; ++eb) {
+                    if (P.eg[eb] != bj) continue;
+                    const EdgeLds& Lb = el[eb];
+                    double d = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * Lb.Xg[jj * 6 + k];
+                    v -= d;
+                    if (ea == eb) v += La.Hgg[ii * 6 + jj];
+                }
+            }
+        } else if (t < ntri + 2 * m) {
+            const int u = t - ntri, w = u / m, i = u % m, bi = i / 6, ii = i % 6;
+            for (int ea = 0; ea < ne; ++ea) {
+                if (P.eg[ea] != bi) continue;
+                const EdgeLds& La = el[ea];
+                if (w == 0) {
+                    double d = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * z[k];
+                    v += La.gg[ii] - d;
+                } else {
+                    v += La.gg[ii];
+                }
+            }
+        } else {
+            v = P.nrm[t - ntri - 2 * m];
+        }
+        st_sc1(cv + t, v);
+    }
+    STAMP(8);
+    // ---- level 1: the last photo of a group sums the group in photo order
+    const int G = a.group_size, grp = photo / G, g0 = grp * G;
+    const int gn = min(G, (int)gridDim.x - g0);
+    if (!arrive_last_sc1(a.cnt + grp, gn)) { RSTAMP(15); return; }
+    STAMP(9);
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        v = sum_sc1(a.contrib + (size_t)g0 * Lc + t, gn, Lc);
+        st_sc1(a.gsum + (size_t)grp * Lc + t, v);
+    }
+    STAMP(10);
+    // ---- level 2: the last group sums the groups in order -> packed system
+    if (!arrive_last_sc1(a.cnt + a.n_groups, a.n_groups)) { RSTAMP(15); return; }
+    STAMP(11);
+    double* S = smem;            // the edge records are dead: m*m + m doubles for the solve
+    double* rr = smem + m * m;
+    __shared__ double nrm2[2];
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        v = sum_sc1(a.gsum + t, a.n_groups, Lc);
+        if (t < ntri) {
+            int i, j;
+            packed_ij(t, m, i, j);
+            S[i * m + j] = v;
+            S[j * m + i] = v;
+        } else if (t < ntri + m) {
+            rr[t - ntri] = v;
+        } else if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
+            const int w = t - ntri - 2 * m;
+            if (st->iter > 0) {
+                if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
+            } else {
+                v = 0.0;
+            }
+            nrm2[w] = v;
+        }
+        a.packed[t] = v;
+    }
+    if (!a.fuse_solve) { RSTAMP(15); return; }
+    __syncthreads();
+    STAMP(12);
+    solve_global(a.solve, S, rr, nrm2[0], nrm2[1]);
+    STAMP(13);
+    RSTAMP(15);
 }
 
 // ---------------------------------------------------------------- global solve (one workgroup)
@@ -705,10 +901,10 @@ __device__ __forceinline__ double sub_sum(double v, int tpr) {
     return v;
 }
 
-// Gauss-Jordan of [S | r] (m x (m+1), m <= 30) by one wavefront with the matrix in registers: lane j
-// owns column j (lane m owns r), pivot columns are broadcast with v_readlane (uniform lane
-// index), every loop is unrolled at compile time (MM >= m).  No LDS traffic, no barriers.
-// Writes delta_i = r_i / S_ii into r[].
+// Gauss-Jordan of [S | r] (m x (m+1), m <= 30) by one wavefront with the matrix in registers:
+// lane i owns row i.  Step k broadcasts only row k right of the pivot (m - k values, v_readlane
+// with a compile-time lane) -- about m^2/2 broadcasts in all -- and every lane i != k eliminates
+// its column-k entry.  S is SPD: no pivoting.  Writes delta_i = r_i / S_ii into r[].
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const unsigned long long b = __double_as_longlong(v);
     const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
@@ -717,50 +913,47 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
 }
 
 template <int MM>
-__device__ __forceinline__ void gj_wave(const double* S, double* r, int m, int lane, int* err) {
-    // every load address is in range for every lane (nothing speculated past the LDS arrays):
-    // lanes >= m read column 0 / r[0] and are masked to 0 afterwards
-    const int lc = lane < m ? lane : 0;
-    double col[MM];
+__device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int lane, int* err) {
+    // every load address is in range for every lane: lanes >= m read row 0 and stay idle
+    const int li = lane < m ? lane : 0;
+    double row[MM];
 #pragma unroll
-    for (int i = 0; i < MM; ++i) {
-        const int ii = i < m ? i : 0;
-        const double vs = S[ii * m + lc];
-        const double vr = r[ii];
-        col[i] = (i < m && lane <= m) ? (lane < m ? vs : vr) : 0.0;
-    }
+    for (int j = 0; j < MM; ++j) row[j] = S[li * m + (j < m ? j : 0)];
+    double rr = r[li], dii = 1.0;
+    bool bad = false;
 #pragma unroll
     for (int k = 0; k < MM; ++k) {
         if (k >= m) break;
-        const double piv = readlane_f64(col[k], k);
-        if (!(piv > 0.0) && lane == 0) atomicOr(err, 2);
-        const double f = col[k] / (piv > 0.0 ? piv : 1.0);
+        const double piv = readlane_f64(row[k], k);
+        bad |= !(piv > 0.0);
+        const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
+        if (lane == k) dii = piv;
+        const double f = lane == k ? 0.0 : row[k] * ip;
 #pragma unroll
-        for (int i = 0; i < MM; ++i)
-            if (i != k) col[i] -= readlane_f64(col[i], k) * f;
+        for (int j = k + 1; j < MM; ++j) {
+            if (j >= m) break;
+            row[j] -= f * readlane_f64(row[j], k);
+        }
+        rr -= f * readlane_f64(rr, k);
     }
-    // lane m holds the eliminated r; divide by the diagonal (lane i's col[i])
-#pragma unroll
-    for (int i = 0; i < MM; ++i) {
-        if (i >= m) break;
-        const double dii = readlane_f64(col[i], i);
-        if (lane == m) r[i] = col[i] / dii;
-    }
+    if (bad && lane == 0) atomicOr(err, 2);
+    if (lane < m) r[lane] = rr / dii;
 }
 
 __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err) {
     switch (m) {
-#define GJ(M) case M: gj_wave<M>(S, r, m, lane, err); break;
+#define GJ(M) case M: gj_rows<M>(S, r, m, lane, err); break;
         GJ(6) GJ(12) GJ(18) GJ(24) GJ(30)
 #undef GJ
         default: break;
     }
 }
 
-__device__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
+__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
     State* st = a.state;
     const int m = a.m, tid = threadIdx.x;
     __shared__ int stop;
+    __shared__ double s_alpha;
     if (tid == 0) {
         const int k = st->iter;
         double change = 1.0;
@@ -775,15 +968,18 @@ __device__ void solve_global(const SolveCtx& a, double* S, double* r, double nor
         stop = s;
         if (s) st->done = 1;
         st->pending = 0;   // this step's k_linearize has applied the previous update
-        st->alpha = a.do_update ? (k < a.n_alpha ? a.alpha[k] : pow(0.95, (double)k + 1.0)) : 0.0;
+        const double alpha = a.do_update ? (k < a.n_alpha ? a.alpha[k] : pow(0.95, (double)k + 1.0)) : 0.0;
+        st->alpha = alpha;
+        s_alpha = alpha;
+    } else if (m <= 30 && tid >= 64 && tid < 128) {
+        // speculative: the elimination does not depend on the stop test (its result is unused
+        // when the loop stops), so wave 1 runs it while wave 0 loads the state
+        gj_dispatch(S, r, m, tid - 64, &st->error);
     }
     __syncthreads();
     if (stop) return;
     STAMPP(a.stamps, 8, 4);
-    if (m <= 30) {
-        if (tid < 64) gj_dispatch(S, r, m, tid, &st->error);
-        __syncthreads();
-    } else {
+    if (m > 30) {
         // ---- Gauss-Jordan elimination of [S | r] without row scaling (S is SPD: no pivoting).
         // Step k updates rows i != k, columns j > k and r from the (unchanged) pivot row/column, so
         // nothing read in step k is written in step k: one barrier per step, no cross-lane
@@ -813,7 +1009,7 @@ __device__ void solve_global(const SolveCtx& a, double* S, double* r, double nor
     if (tid < 64) {
         const int lane = tid;
         // global block: delta, update, norm partials (identical on every rank)
-        const double alpha = st->alpha;
+        const double alpha = s_alpha;
         double g2 = 0.0, x2 = 0.0;
         for (int i = lane; i < m; i += 64) {
             const double d = r[i];
@@ -940,11 +1136,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             int i, j, w = 0, blk;
             const double* src;
             if (t < ntri) {
-                // packed upper index -> (i, j): row i holds m - i entries
-                i = (int)((2.0 * m + 1.0 - sqrt((2.0 * m + 1.0) * (2.0 * m + 1.0) - 8.0 * t)) * 0.5);
-                while (i > 0 && i * m - i * (i - 1) / 2 > t) --i;
-                while ((i + 1) * m - (i + 1) * i / 2 <= t) ++i;
-                j = i + (t - (i * m - i * (i - 1) / 2));
+                packed_ij(t, m, i, j);
                 const int b1 = i / 6, b2 = j / 6;
                 blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
                 src = a.item_out + (i % 6) * 6 + (j % 6);
@@ -1170,14 +1362,15 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     return hipGetLastError();
 }
 
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams) {
-    return (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) + 18 * sizeof(double) * (size_t)n_cams;
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused) {
+    const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) + 18 * sizeof(double) * (size_t)n_cams;
+    return fused ? std::max(lin, (size_t)(m * m + m) * sizeof(double)) : lin;
 }
 
 size_t mcc_solve_shmem(int m) { return (size_t)(m * m + m) * sizeof(double); }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams);
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
         case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
@@ -1185,9 +1378,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m) {
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused) {
     hipError_t err = hipSuccess;
-    const size_t shmem = mcc_lin_shmem(max_epp, n_cams);
+    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
         for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),

@@ -4,6 +4,11 @@ stamps at phase boundaries; cdna guide section 7 'In-kernel stamps').  Never quo
 run time: read its shares.
 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_stamps.py [config] [views]
+
+Slots per workgroup (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written,
+9 group ticket won, 10 group sum written, 11 final ticket won, 12 system assembled, 13 solved
+(fused step); 14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit.  s_memtime is per XCD,
+so only differences within one workgroup are meaningful; the cross-workgroup timeline uses 14/15.
 """
 import os
 import sys
@@ -16,6 +21,10 @@ from multi_camera_calibration_amd import api, rig  # noqa: E402
 PHASES = ["pending-update", "prologue", "sweep(wave0)", "reduce+barrier", "chain+H", "photo-chol", "Y/out"]
 
 
+def med(v):
+    return f"median {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}" if len(v) else "n/a"
+
+
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "config2"
     views = int(sys.argv[2]) if len(sys.argv) > 2 else None
@@ -25,37 +34,43 @@ def main():
     ba.step(20)
     ba.synchronize()
     ba.stamps()          # arm
-    ba.step(3)
+    ba.step(1)
     ba.synchronize()
     raw = ba.stamps().reshape(-1)
     nv = max(p.n_photos, 1)
-    lin = raw[:16 * nv].reshape(nv, 16).astype(np.float64)
+    s = raw[:16 * nv].reshape(nv, 16).astype(np.float64)
     sch = raw[16 * nv:].reshape(-1, 8).astype(np.float64)
-    s = lin
-    t0 = s[:, 0]
-    ok = t0 > 0
-    s = s[ok]
-    # stamp 3 is taken per sweep round by wave 0, 4 after each chain round: use the last values
+    s = s[s[:, 0] > 0]
     d = np.diff(s[:, :8], axis=1)
-    print(f"{cfg}: {ok.sum()} workgroups stamped")
+    print(f"{cfg}: {len(s)} workgroups stamped (s_memtime ticks)")
     for k, name in enumerate(PHASES):
-        col = d[:, k]
-        print(f"  {name:16s} median {np.median(col):9.0f}  p90 {np.percentile(col, 90):9.0f}  (s_memtime ticks)")
-    tot = s[:, 7] - s[:, 0]
-    print(f"  {'total':16s} median {np.median(tot):9.0f}  p90 {np.percentile(tot, 90):9.0f}")
-    span = s[:, 7].max() - s[:, 0].min()
-    print(f"  kernel span (first start -> last end): {span:.0f} ticks; start spread {s[:, 0].max() - s[:, 0].min():.0f}")
+        print(f"  {name:16s} {med(d[:, k])}")
+    print(f"  {'linearize total':16s} {med(s[:, 7] - s[:, 0])}")
+    fused = (s[:, 8] > 0).any()
+    if fused:
+        print(f"  {'contribution':16s} {med(s[:, 8] - s[:, 7])}")
+        g = s[s[:, 9] > 0]
+        print(f"  group reducers: {len(g)}; ticket {med(g[:, 9] - g[:, 8])}; group sum {med(g[:, 10] - g[:, 9])}")
+        f = s[s[:, 11] > 0]
+        if len(f):
+            F = f[0]
+            print(f"  final: ticket {F[11] - F[10]:.0f}, assemble {F[12] - F[11]:.0f}, solve {F[13] - F[12]:.0f}")
+    r0, r1 = s[:, 14], s[:, 15]
+    ok = r1 > 0
+    if ok.any():
+        t0 = r0.min()
+        print(f"  timeline (us, 100 MHz): starts spread {(r0.max() - t0) / 100:.2f}; "
+              f"exit median {(np.median(r1[ok]) - t0) / 100:.2f}; last exit {(r1[ok].max() - t0) / 100:.2f}")
+        print(f"  workgroup residency (us): {med((r1[ok] - r0[ok]) / 100)}")
     ok = sch[:, 0] > 0
-    it = sch[ok]
-    print(f"k_schur: {ok.sum()} workgroups; item compute median {np.median(it[:, 1] - it[:, 0]):.0f}, "
-          f"ticket median {np.median(it[:, 2] - it[:, 1]):.0f} (non-last rows have 0 in slot 2)")
-    last = sch[sch[:, 3] > 0]
-    if len(last):
-        L = last[0]
-        names = ["start", "items", "acquire", "assembly", "stoptest", "crout", "trisolve", "end"]
-        print("  last arriver: " + ", ".join(f"{names[k]}->{names[k+1]} {L[k+1]-L[k]:.0f}" for k in range(7)))
-        print(f"  kernel span {sch[ok, 0].min():.0f} -> {L[7]:.0f}: {L[7] - sch[ok, 0].min():.0f} ticks; "
-              f"last item start {sch[ok, 0].max() - sch[ok, 0].min():.0f} after the first")
+    if ok.any():
+        it = sch[ok]
+        print(f"k_schur: {ok.sum()} workgroups; item compute {med(it[:, 1] - it[:, 0])}")
+        last = sch[sch[:, 3] > 0]
+        if len(last):
+            L = last[0]
+            names = ["start", "items", "acquire", "assembly", "stoptest", "solve", "update", "end"]
+            print("  last arriver: " + ", ".join(f"{names[k]}->{names[k+1]} {L[k+1]-L[k]:.0f}" for k in range(7)))
 
 
 if __name__ == "__main__":
