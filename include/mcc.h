@@ -130,7 +130,8 @@ int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
 /* diagnostic build only (libmcc_diag.so, -DMCC_DIAG): first call arms per-phase s_memtime
- * stamps of k_linearize, later calls copy [16 * n_photos] stamps out (others: MCC_EINVAL) */
+ * stamps of k_linearize, later calls copy [32 * n_photos] stamps (then k_schur's [8 * grid]) out
+ * (others: MCC_EINVAL) */
 int mcc_debug_stamps(mcc_problem *p, long long *out, int n);
 /* static facts about the problem for roofline accounting */
 int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges,

@@ -235,8 +235,9 @@ class BundleAdjuster:
         return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
 
     def stamps(self):
-        """libmcc_diag.so only: first call arms, later calls return [n_photos, 16] s_memtime stamps."""
-        out = np.zeros(16 * max(self.prob.n_photos, 1) + 8 * 65536, np.int64)
+        """libmcc_diag.so only: first call arms, later calls return [n_photos, 32] s_memtime stamps
+        followed by k_schur's [workgroups, 8]."""
+        out = np.zeros(32 * max(self.prob.n_photos, 1) + 8 * 65536, np.int64)
         _check(lib().mcc_debug_stamps(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), out.size),
                "mcc_debug_stamps")
         return out

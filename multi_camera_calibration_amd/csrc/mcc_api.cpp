@@ -112,6 +112,7 @@ struct mcc_problem {
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
+    int max_cpp = 1;   // most corners of one photo
     hipStream_t stream = nullptr;
 
     // host-side maps
@@ -123,7 +124,7 @@ struct mcc_problem {
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum;
-    DevBuf<int> photo_ptr, edge_gblock, block_items, edge_photo, counter, cnt;
+    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
@@ -158,6 +159,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     LinArgs la{};
     la.state = p->state.p;
     la.photo_ptr = p->photo_ptr.p;
+    la.photo_corner = p->photo_corner.p;
+    la.max_cpp = p->max_cpp;
     la.edge_info = p->edge_info.p;
     la.obj_x = p->obj_x.p; la.obj_y = p->obj_y.p; la.obj_z = p->obj_z.p;
     la.img_u = p->img_u.p; la.img_v = p->img_v.p;
@@ -211,7 +214,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.packed = p->packed.p;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = multi ? 0 : 1;
     sa.solve = solve_ctx(p, do_update);
-    sa.stamps = p->stamps.p ? p->stamps.p + 16 * (size_t)std::max(p->V, 1) : nullptr;
+    sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
     if (multi) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
@@ -409,6 +412,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         else gblock[de] = d->edge_cam[e] - 1;
         off += n;
     }
+    std::vector<int> photo_corner(V + 1, 0);
+    for (int v = 0; v < V; ++v) {
+        photo_corner[v + 1] = photo_corner[v];
+        for (int de = photo_ptr[v]; de < photo_ptr[v + 1]; ++de) photo_corner[v + 1] += info[de].w;
+        p->max_cpp = std::max(p->max_cpp, photo_corner[v + 1] - photo_corner[v]);
+    }
 
     // ---- Schur pair lists grouped by camera-pair block, chunked into work items
     const int nb = p->m / 6;
@@ -478,6 +487,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->edge_gblock.upload(gblock.data(), E));
     HIPC(p->edge_photo.upload(ephoto.data(), E));
     HIPC(p->photo_ptr.upload(photo_ptr.data(), V + 1));
+    HIPC(p->photo_corner.upload(photo_corner.data(), V + 1));
     HIPC(p->K.upload(d->K, 9 * C));
     HIPC(p->D.upload(d->D, (size_t)d->nd * C));
     std::vector<float> xi(C, 0.f);
@@ -521,8 +531,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
-    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused) > 160 * 1024) return bail(fail(MCC_EINVAL, "too many edges per photo"));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused));
+    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused, p->max_cpp) > 160 * 1024)
+        return bail(fail(MCC_EINVAL, "too many edges / corners per photo for the LDS staging"));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused, p->max_cpp));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -545,7 +556,7 @@ void mcc_destroy(mcc_problem* p) {
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Lp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
-    p->photo_ptr.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release();
+    p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
@@ -686,7 +697,7 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     if (!p->stamps.p) {
-        const size_t n_st = 16 * (size_t)std::max(p->V, 1) + 8 * (size_t)(p->n_items + p->n_norm_chunks);
+        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + 8 * (size_t)(p->n_items + p->n_norm_chunks);
         HIPCHK(p->stamps.alloc(n_st));
         HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
         for (auto& g : p->gexec)

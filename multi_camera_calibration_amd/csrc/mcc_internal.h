@@ -7,6 +7,8 @@
 
 namespace mcc {
 
+constexpr int kStampStride = 32;   // MCC_DIAG: s_memtime / s_memrealtime slots per k_linearize workgroup
+
 // Device-resident loop state of optimizeExtrinsics (src/multicalib.cpp:468-507).
 struct State {
     int iter;         // completed updates k
@@ -34,6 +36,8 @@ struct SolveCtx {
 struct LinArgs {
     State* state;
     const int* photo_ptr;     // [V+1] photo-major edge ranges
+    const int* photo_corner;  // [V+1] photo-major corner ranges (corners of a photo are contiguous)
+    int max_cpp;              // most corners of one photo (LDS staging)
     const int4* edge_info;    // [E] {cam, side, corner_off, n}
     const float* obj_x; const float* obj_y; const float* obj_z;   // [corners] photo-major
     const float* img_u; const float* img_v;
@@ -114,9 +118,9 @@ struct ErrArgs {
 }  // namespace mcc
 
 // launch wrappers (mcc_kernels.hip)
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused);
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);

@@ -36,13 +36,26 @@ namespace mcc {
 #else
 #define STAMPP(ptr, stride, k) do { } while (0)
 #endif
-#define STAMP(k) STAMPP(a.stamps, 16, k)
+#define STAMP(k) STAMPP(a.stamps, kStampStride, k)
+// stamp into an explicit slot row (ptr already points at this workgroup's row), by thread `who`
+#ifdef MCC_DIAG
+#define SSTAMP(ptr, k, who)                                                                        \
+    do {                                                                                           \
+        if (threadIdx.x == (who) && (ptr)) {                                                       \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+            (ptr)[k] = (long long)__builtin_amdgcn_s_memtime();                                    \
+            __builtin_amdgcn_sched_barrier(0);                                                     \
+        }                                                                                          \
+    } while (0)
+#else
+#define SSTAMP(ptr, k, who) do { } while (0)
+#endif
 // chip-wide 100 MHz clock (s_memtime is per XCD): cross-workgroup timelines
 #ifdef MCC_DIAG
 #define RSTAMP(k)                                                                                  \
     do {                                                                                           \
         if (threadIdx.x == 0 && a.stamps)                                                          \
-            a.stamps[16 * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+            a.stamps[kStampStride * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define RSTAMP(k) do { } while (0)
@@ -74,6 +87,13 @@ __device__ __forceinline__ int bfly_index(int lane) {
     return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
            ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
 }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const unsigned long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 // fixed-order full wave sum (xor butterfly)
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -82,6 +102,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 constexpr int kLpStride = 42;   // per photo: L (6x6, lower) + 1/L_ii
+constexpr int kCamStride = 24;  // LDS camera table row: R (9), Jl (9), T (3), pad
+constexpr int kIntrStride = 20; // LDS intrinsics row: fx, fy, cx, cy, skew, xi, k[12], pad
 
 // ---------------------------------------------------------------- per-edge LDS record
 struct EdgeLds {
@@ -120,14 +142,17 @@ __device__ __forceinline__ void store_G(double* G, const double* Grr, const doub
 // cameras and the double-side transform come from the workgroup's LDS tables (phase 0).
 struct PhotoLds {
     double xp[6];        // photo parameters (double of the float32 state)
+    double xo[6];        // photo parameters before the pending update (float32 values)
     double R1[9], Jr1[9];
     double Rds[9], Jrds[9], dst[3], pad0;
-    double Lo[42], zo[6], tk[6];     // pending-update staging (L, 1/L_ii, z)
     double Hs[36], gs[6], Lm[36], z[6], il[6];
-    double dg[128];      // global-block delta of the previous solve
+    double dgl[128];     // global-block delta of the previous solve (pending update)
     double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
     int eg[64];          // global block of each edge of the photo or -1 (fused step)
-    // followed by the camera table: [C][18] = {R (9), Jl (9)}
+    int bn[8];           // per camera block: number of the photo's edges in it (fused step)
+    unsigned char bl[5][64];   // per camera block: those edges in edge order
+    // followed by the camera table [C][kCamStride], the intrinsics [C][kIntrStride] and the
+    // photo's corners [5][max_cpp] (float)
 };
 static_assert(sizeof(PhotoLds) % 16 == 0, "PhotoLds alignment");
 
@@ -183,24 +208,12 @@ __device__ __forceinline__ void finish_pose(const double* om, const double* T, d
 }
 
 template <int MODEL>
-__device__ void edge_prologue(const LinArgs& a, const PhotoLds& P, const double* ctab, int e, EdgeLds& L) {
-    const int4 info = a.edge_info[e];
-    const int cam = info.x, side = info.y;
+__device__ void edge_prologue(const PhotoLds& P, const double* ctab, EdgeLds& L) {
+    const int cam = L.cam, side = L.side;
     const double T1[3] = {P.xp[3], P.xp[4], P.xp[5]};
-    double T2[3];
-    if (MODEL == MCC_MODEL_DOUBLESIDE) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) T2[k] = a.cam_rt[6 * cam + 3 + k];
-    } else if (cam == 0) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) T2[k] = 0.0;   // src/mymulticalib.cpp:721-725
-    } else {
-        const float* xc = a.x + 6 * (cam - 1);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) T2[k] = xc[3 + k];
-    }
-    const double* R2 = ctab + 18 * cam;
+    const double* R2 = ctab + kCamStride * cam;
     const double* Jl2 = R2 + 9;
+    const double* T2 = R2 + 18;
     Motion f;
     double th3, s3, c3;
     compose(P.R1, P.Jr1, T1, R2, Jl2, T2, f, th3, s3, c3);
@@ -248,11 +261,233 @@ __device__ void edge_prologue(const LinArgs& a, const PhotoLds& P, const double*
             L.has_global = cam != 0;
         }
     }
-    L.cam = cam;
-    L.side = side;
-    L.off = info.z;
-    L.n = info.w;
-    L.edge = e;
+}
+
+
+// ---------------------------------------------------------------- wave-cooperative edge prologue
+// The same chain as edge_prologue (src/mymulticalib.cpp:468-614, src/multicalib.cpp:717-824,
+// src/doubleSide.cpp:288-430) computed by the wave that sweeps the edge: lanes own matrix
+// entries (3-term dot products instead of one lane doing every 3x3 product), while the rotation
+// logs / Rodrigues / Jacobian coefficients every entry needs are evaluated by all lanes.  Value
+// paths keep OpenCV's operation order with contraction off.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ double dot3_nc(double a0, double b0, double a1, double b1, double a2, double b2) {
+#pragma clang fp contract(off)
+    return a0 * b0 + a1 * b1 + a2 * b2;
+}
+__device__ __forceinline__ double add_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+// row i (runtime) of I + s1 [w]x + s2 [w]x^2
+__device__ __forceinline__ void so3_poly_row(const double* w, double s1, double s2, int i, double* row) {
+    double M[9];
+    so3_poly(w, s1, s2, M);
+    row[0] = i == 0 ? M[0] : (i == 1 ? M[3] : M[6]);
+    row[1] = i == 0 ? M[1] : (i == 1 ? M[4] : M[7]);
+    row[2] = i == 0 ? M[2] : (i == 1 ? M[5] : M[8]);
+}
+// column j (runtime) of I + s1 [w]x + s2 [w]x^2
+__device__ __forceinline__ void so3_poly_col(const double* w, double s1, double s2, int j, double* col) {
+    double M[9];
+    so3_poly(w, s1, s2, M);
+    col[0] = j == 0 ? M[0] : (j == 1 ? M[1] : M[2]);
+    col[1] = j == 0 ? M[3] : (j == 1 ? M[4] : M[5]);
+    col[2] = j == 0 ? M[6] : (j == 1 ? M[7] : M[8]);
+}
+// so3_jac's coefficients: J = I + sign*a [w]x + b [w]x^2
+__device__ __forceinline__ void jac_coef(double th, double s, double c, double& a, double& b) {
+    const double t2 = th * th;
+    if (th < 1e-2) {
+        a = 0.5 - t2 * (1.0 / 24.0) + t2 * t2 * (1.0 / 720.0);
+        b = 1.0 / 6.0 - t2 * (1.0 / 120.0) + t2 * t2 * (1.0 / 5040.0);
+    } else {
+        a = (1.0 - c) / t2;
+        b = (th - s) / (t2 * th);
+    }
+}
+// so3_jac_inv's coefficient: J^-1 = I - sign*0.5 [w]x + ci [w]x^2
+__device__ __forceinline__ double jinv_coef(double th, double s, double c) {
+    const double t2 = th * th;
+    if (th < 1e-2) return 1.0 / 12.0 + t2 * (1.0 / 720.0) + t2 * t2 * (1.0 / 30240.0);
+    return 1.0 / t2 - (1.0 + c) / (2.0 * th * s);
+}
+// row i of -[q]x
+__device__ __forceinline__ void negskew_row(const double* q, int i, double* row) {
+    row[0] = i == 0 ? 0.0 : (i == 1 ? -q[2] : q[1]);
+    row[1] = i == 0 ? q[2] : (i == 1 ? 0.0 : -q[0]);
+    row[2] = i == 0 ? -q[1] : (i == 1 ? q[0] : 0.0);
+}
+
+template <int MODEL>
+__device__ __forceinline__ void edge_prologue_wave(const PhotoLds& P, const double* ctab, EdgeLds& L, int lane) {
+    const int cam = L.cam, side = L.side;
+    const double* R2 = ctab + kCamStride * cam;
+    const double* Jl2 = R2 + 9;
+    const double* T2 = R2 + 18;
+    double* X = L.Xp;    // R3 [0..8], T3 [9..11], q [12..14]; back: Rb [18..26], Tb [27..29], qb [30..32]
+    double* W = L.Xg;    // A1 [0..8], A2 [9..17], B2 [18..26]; back: A1b [27..35]
+    double* Wb = L.Hgp;  // back: A2b [0..8], B2b [9..17]
+    // ---- compose_motion(photo, camera) values: R3 = R2 R1, q = R2 T1, T3 = q + T2
+    if (lane < 9) {
+        const int i = lane / 3, j = lane % 3;
+        X[lane] = dot3_nc(R2[i * 3], P.R1[j], R2[i * 3 + 1], P.R1[3 + j], R2[i * 3 + 2], P.R1[6 + j]);
+    } else if (lane < 12) {
+        const int i = lane - 9;
+        const double q = dot3_nc(R2[i * 3], P.xp[3], R2[i * 3 + 1], P.xp[4], R2[i * 3 + 2], P.xp[5]);
+        X[12 + i] = q;
+        X[9 + i] = add_nc(q, T2[i]);
+    }
+    wave_sync_lds();
+    double om[3], th, sn, cs;
+    {
+        double R3[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R3[k] = X[k];
+        rodrigues_m2v(R3, om, th, sn, cs);
+    }
+    // ---- A1 = Jr^-1(om3) Jr(om1), A2 = Jl^-1(om3) Jl(om2), B2 = -[q]x Jl(om2)
+    if (lane < 27) {
+        const int blk = lane / 9, e = lane % 9, i = e / 3, j = e % 3;
+        double row[3];
+        if (blk < 2) {
+            so3_poly_row(om, blk == 0 ? 0.5 : -0.5, jinv_coef(th, sn, cs), i, row);
+        } else {
+            const double q[3] = {X[12], X[13], X[14]};
+            negskew_row(q, i, row);
+        }
+        const double* B = blk == 0 ? P.Jr1 : Jl2;
+        W[lane] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+    }
+    if (side != MCC_BACK) {
+        wave_sync_lds();
+        // float32 composed pose (src/mymulticalib.cpp:546-553), its Rodrigues and Jl
+        double rf[3], Tf[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)om[k]; Tf[k] = (double)(float)X[9 + k]; }
+        Rot rp;
+        rodrigues_near(rf, th, sn, cs, rp);
+        double ja, jb;
+        jac_coef(rp.th, rp.s, rp.c, ja, jb);
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) L.R[k] = rp.R[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) L.T[k] = Tf[k];
+            L.has_global = MODEL == MCC_MODEL_DOUBLESIDE ? 0 : (cam != 0);
+        }
+        // Gp = [[Jl A1, 0], [0, R2]];  Gg = [[Jl A2, 0], [B2, I]]  (DoubleSide front: 0,
+        // src/doubleSide.cpp:335-336)
+        for (int e = lane; e < 72; e += 64) {
+            const int w = e / 36, r = (e % 36) / 6, c = e % 6;
+            double v;
+            if (r < 3 && c < 3) {
+                double row[3];
+                so3_poly_row(rf, ja, jb, r, row);
+                const double* M = w == 0 ? W : W + 9;
+                v = row[0] * M[c] + row[1] * M[3 + c] + row[2] * M[6 + c];
+                if (w == 1 && MODEL == MCC_MODEL_DOUBLESIDE) v = 0.0;
+            } else if (r < 3) {
+                v = 0.0;
+            } else if (c < 3) {
+                v = (w == 1 && MODEL != MCC_MODEL_DOUBLESIDE) ? W[18 + (r - 3) * 3 + c] : 0.0;
+            } else {
+                v = w == 0 ? R2[(r - 3) * 3 + c - 3]
+                           : (MODEL == MCC_MODEL_DOUBLESIDE ? 0.0 : (r == c ? 1.0 : 0.0));
+            }
+            (w == 0 ? L.Gp : L.Gg)[r * 6 + c] = v;
+        }
+        return;
+    }
+    // ---- BACK: compose_motion(ds, photofront), src/mymulticalib.cpp:503-518,
+    // src/doubleSide.cpp:320-328; R(om_front) is the FP64 composed rotation R3
+    double fa, fb;
+    jac_coef(th, sn, cs, fa, fb);   // Jlf = Jl(om_front)
+    if (lane < 9) {
+        const int i = lane / 3, j = lane % 3;
+        X[18 + lane] = dot3_nc(X[i * 3], P.Rds[j], X[i * 3 + 1], P.Rds[3 + j], X[i * 3 + 2], P.Rds[6 + j]);
+    } else if (lane < 12) {
+        const int i = lane - 9;
+        const double q = dot3_nc(X[i * 3], P.dst[0], X[i * 3 + 1], P.dst[1], X[i * 3 + 2], P.dst[2]);
+        X[30 + i] = q;
+        X[27 + i] = add_nc(q, X[9 + i]);
+    }
+    wave_sync_lds();
+    double omb[3], thb, snb, csb;
+    {
+        double Rb[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rb[k] = X[18 + k];
+        rodrigues_m2v(Rb, omb, thb, snb, csb);
+    }
+    // A1b = Jr^-1(omb) Jr(ds), A2b = Jl^-1(omb) Jlf, B2b = -[qb]x Jlf
+    if (lane < 27) {
+        const int blk = lane / 9, e = lane % 9, i = e / 3, j = e % 3;
+        double row[3], col[3];
+        if (blk < 2) {
+            so3_poly_row(omb, blk == 0 ? 0.5 : -0.5, jinv_coef(thb, snb, csb), i, row);
+        } else {
+            const double q[3] = {X[30], X[31], X[32]};
+            negskew_row(q, i, row);
+        }
+        if (blk == 0) {
+            col[0] = P.Jrds[j]; col[1] = P.Jrds[3 + j]; col[2] = P.Jrds[6 + j];
+        } else {
+            so3_poly_col(om, fa, fb, j, col);
+        }
+        const double v = row[0] * col[0] + row[1] * col[1] + row[2] * col[2];
+        if (blk == 0) W[27 + e] = v;
+        else Wb[(blk - 1) * 9 + e] = v;
+    }
+    wave_sync_lds();
+    double rf[3], Tf[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)omb[k]; Tf[k] = (double)(float)X[27 + k]; }
+    Rot rp;
+    rodrigues_near(rf, thb, snb, csb, rp);
+    double ja, jb;
+    jac_coef(rp.th, rp.s, rp.c, ja, jb);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) L.R[k] = rp.R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) L.T[k] = Tf[k];
+        L.has_global = MODEL == MCC_MODEL_DOUBLESIDE ? 1 : (cam != 0);
+    }
+    // Gp = [[Jl A2b A1, 0], [B2b A1, R2]];  Gg (MyMulti, hazard A12) = [[Jl A2b A2, 0], [B2b A2, I]];
+    // Gg (DoubleSide ds block) = [[Jl A1b, 0], [0, R_front]]
+    for (int e = lane; e < 72; e += 64) {
+        const int w = e / 36, r = (e % 36) / 6, c = e % 6;
+        const bool ds = w == 1 && MODEL == MCC_MODEL_DOUBLESIDE;
+        const double* M = w == 0 ? W : W + 9;   // A1 (photo) / A2 (camera)
+        double v;
+        if (r < 3 && c < 3) {
+            double row[3];
+            so3_poly_row(rf, ja, jb, r, row);
+            if (ds) {
+                v = row[0] * W[27 + c] + row[1] * W[30 + c] + row[2] * W[33 + c];
+            } else {
+                v = 0.0;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double am = Wb[k * 3] * M[c] + Wb[k * 3 + 1] * M[3 + c] + Wb[k * 3 + 2] * M[6 + c];
+                    v += row[k] * am;
+                }
+            }
+        } else if (r < 3) {
+            v = 0.0;
+        } else if (c < 3) {
+            const int i = r - 3;
+            v = ds ? 0.0 : Wb[9 + i * 3] * M[c] + Wb[9 + i * 3 + 1] * M[3 + c] + Wb[9 + i * 3 + 2] * M[6 + c];
+        } else {
+            v = w == 0 ? R2[(r - 3) * 3 + c - 3] : (ds ? X[(r - 3) * 3 + c - 3] : (r == c ? 1.0 : 0.0));
+        }
+        (w == 0 ? L.Gp : L.Gg)[r * 6 + c] = v;
+    }
 }
 
 // ---------------------------------------------------------------- per-corner models
@@ -453,15 +688,17 @@ __device__ __forceinline__ void packed_ij(int t, int m, int& i, int& j) {
     j = row + rem;
 }
 
-// sum_{q < n} p[q * stride] in q order with sc1 loads issued 8 at a time (in flight together)
+// sum_{q < n} p[q * stride] in q order with sc1 loads issued 24 at a time (one memory round
+// trip for the group sizes of a few hundred to ~600 photos)
 __device__ __forceinline__ double sum_sc1(const double* p, int n, size_t stride) {
+    constexpr int B = 24;
     double v = 0.0;
-    for (int q0 = 0; q0 < n; q0 += 8) {
-        double b[8];
+    for (int q0 = 0; q0 < n; q0 += B) {
+        double b[B];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) b[u] = ld_sc1(p + (size_t)min(q0 + u, n - 1) * stride);
+        for (int u = 0; u < B; ++u) b[u] = ld_sc1(p + (size_t)min(q0 + u, n - 1) * stride);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v += q0 + u < n ? b[u] : 0.0;
+        for (int u = 0; u < B; ++u) v += q0 + u < n ? b[u] : 0.0;
     }
     return v;
 }
@@ -473,48 +710,83 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 template <int MODEL, bool RATIONAL, bool PRISM>
 __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
-    if (st->done) return;
-    STAMP(0);
-    RSTAMP(14);
     const int photo = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // ---- round trip 1: everything indexed by the photo alone
+    const int done = st->done, pending = st->pending;
+    const double alpha_prev = st->alpha;   // step factor of the pending update
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
+    if (done) return;
+    STAMP(0);
+    RSTAMP(14);
     extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
     PhotoLds& P = *reinterpret_cast<PhotoLds*>(smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double)));
-    double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][18]
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][kCamStride] = {R, Jl, T}
+    double* ktab = ctab + kCamStride * a.n_cams;         // [C][kIntrStride] intrinsics
+    float* cs = reinterpret_cast<float*>(ktab + kIntrStride * a.n_cams);   // [5][max_cpp] corners
+    const int c0 = a.photo_corner[photo];
+    const int ncs = a.photo_corner[photo + 1] - c0;
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
-    const int pending = st->pending;
 
-    // ---- phase 0: stage the pending update's operands (one round trip, all threads) while
-    // wave 1 builds the camera / double-side Rodrigues tables.
-    if (pending) {
-        for (int q = tid; q < 36 * ne; q += blockDim.x) el[q / 36].Xp[q % 36] = a.Y[36 * (size_t)e0 + q];
-        if (tid < 42) P.Lo[tid] = a.Lp[kLpStride * (size_t)photo + tid];   // L (36) + 1/L_ii (6)
-        else if (tid < 48) P.zo[tid - 42] = a.zp[6 * (size_t)photo + tid - 42];
-        for (int q = tid; q < a.global_dim; q += blockDim.x) P.dg[q] = a.dg[q];
-    }
-    if (wave == 1) {
+    // ---- phase 0.  wave 0: photo parameters, pending-update operands (registers);
+    // wave 1: camera / double-side / intrinsics tables; waves 2-3: the photo's corners -> LDS;
+    // every thread < ne: its edge record
+    double part = 0.0, lov = 0.0;
+    float xov = 0.f;
+    if (wave == 0) {
+        if (lane < 6) xov = xg[lane];
+        else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
+        if (pending) {
+            if (lane < 42) lov = a.Lp[kLpStride * (size_t)photo + lane];   // L (36) + 1/L_ii (6)
+            else if (lane < 48) lov = a.zp[6 * (size_t)photo + lane - 42];
+            for (int q = lane; q < a.global_dim; q += 64) P.dgl[q] = a.dg[q];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // lane l < 60: k = l % 6, edges l / 6, l / 6 + 10, ...: sum_i Y_e[i][k] dg_{g(e)}[i]
+            if (lane < 60) {
+                const int k = lane % 6;
+                for (int le = lane / 6; le < ne; le += 10) {
+                    const int g = a.gblock[e0 + le];
+                    if (g < 0) continue;
+                    const double* Ye = a.Y + 36 * (size_t)(e0 + le) + k;
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) part += Ye[6 * i] * P.dgl[6 * g + i];
+                }
+            }
+        }
+    } else if (wave == 1) {
         if (lane < a.n_cams) {
             const int c = lane;
-            double om2[3];
+            double om2[3], T2[3];
             if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) om2[k] = a.cam_rt[6 * c + k];
+                for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * c + k]; T2[k] = a.cam_rt[6 * c + 3 + k]; }
             } else if (c == 0) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) om2[k] = 0.0;
+                for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
             } else {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) om2[k] = a.x[6 * (c - 1) + k];
+                for (int k = 0; k < 3; ++k) { om2[k] = a.x[6 * (c - 1) + k]; T2[k] = a.x[6 * (c - 1) + 3 + k]; }
             }
+            double* kt = ktab + kIntrStride * c;
+            const float* Kc = a.K + 9 * c;
+            kt[0] = Kc[0]; kt[1] = Kc[4]; kt[2] = Kc[2]; kt[3] = Kc[5]; kt[4] = Kc[1];
+            kt[5] = MODEL == MCC_MODEL_OMNI ? (double)a.xi[c] : 0.0;
+            const int nd = a.nd;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) kt[6 + q] = q < nd ? (double)a.D[nd * c + q] : 0.0;
             Rot r2;
             rodrigues_v2m(om2, r2);
             double J[9];
             so3_jac(om2, r2, +1.0, J);
+            double* ct = ctab + kCamStride * c;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) { ctab[18 * c + k] = r2.R[k]; ctab[18 * c + 9 + k] = J[k]; }
+            for (int k = 0; k < 9; ++k) { ct[k] = r2.R[k]; ct[9 + k] = J[k]; }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ct[18 + k] = T2[k];
         } else if (lane == 63 && a.has_back) {
             double dsr[3];
             if (MODEL == MCC_MODEL_DOUBLESIDE) {
@@ -531,55 +803,61 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) { P.Rds[k] = rd.R[k]; P.Jrds[k] = J[k]; }
         }
+    } else {
+        // the photo's corners are contiguous (photo-major layout): stage all five streams
+        for (int q = tid - 128; q < ncs; q += 128) {
+            const size_t c = (size_t)c0 + q;
+            cs[q] = a.obj_x[c];
+            cs[a.max_cpp + q] = a.obj_y[c];
+            cs[2 * a.max_cpp + q] = a.obj_z[c];
+            cs[3 * a.max_cpp + q] = a.img_u[c];
+            cs[4 * a.max_cpp + q] = a.img_v[c];
+        }
     }
-    __syncthreads();
+    for (int le = tid; le < ne; le += blockDim.x) {
+        const int4 info = a.edge_info[e0 + le];
+        EdgeLds& L = el[le];
+        L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
+    }
+    STAMP(16);
     if (wave == 0) {
         if (pending) {
-            // fused back-substitution of the previous step: dp = L^-T (z - sum_e Y_e^T dg_e)
-            if (lane < 6) {
-                const int k = lane;
-                double sacc = P.zo[k];
-                for (int le = 0; le < ne; ++le) {
-                    const int g = a.gblock[e0 + le];
-                    if (g < 0) continue;
+            // fused back-substitution of the previous step: dp = L^-T (z - sum_e Y_e^T dg_e),
+            // operands gathered from wave 0's registers with compile-time v_readlane
+            double t[6];
 #pragma unroll
-                    for (int i = 0; i < 6; ++i) sacc -= el[le].Xp[i * 6 + k] * P.dg[6 * g + i];
-                }
-                P.tk[k] = sacc;
+            for (int q = 0; q < 6; ++q) {
+                double sacc = readlane_f64(lov, 42 + q);
+#pragma unroll
+                for (int j = 0; j < 10; ++j) sacc -= readlane_f64(part, 6 * j + q);
+                t[q] = sacc;
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (int i = 5; i >= 0; --i) {
+                double sacc = t[i];
+#pragma unroll
+                for (int q = i + 1; q < 6; ++q) sacc -= readlane_f64(lov, q * 6 + i) * t[q];
+                t[i] = sacc * readlane_f64(lov, 36 + i);
+            }
+            double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const float G = (float)(alpha_prev * t[q]);   // G = alpha*delta -> CV_32F (:491-496)
+                const float xn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xov), q)) + G;   // x = x + G (:501)
+                if (lane == q) { xg[q] = xn; P.xp[q] = xn; }
+                g2 += (double)G * (double)G;
+                x2 += (double)xn * (double)xn;
+            }
             if (lane == 0) {
-                double t[6];
-#pragma unroll
-                for (int q = 0; q < 6; ++q) t[q] = P.tk[q];
-#pragma unroll
-                for (int i = 5; i >= 0; --i) {
-                    double sacc = t[i];
-#pragma unroll
-                    for (int q = i + 1; q < 6; ++q) sacc -= P.Lo[q * 6 + i] * t[q];
-                    t[i] = sacc * P.Lo[36 + i];
-                }
-                const double alpha = st->alpha;
-                double g2 = 0.0, x2 = 0.0;
-#pragma unroll
-                for (int q = 0; q < 6; ++q) {
-                    const float G = (float)(alpha * t[q]);     // G = alpha*delta -> CV_32F (:491-496)
-                    const float xn = xg[q] + G;                // x = x + G (:501)
-                    xg[q] = xn;
-                    P.xp[q] = xn;
-                    g2 += (double)G * (double)G;
-                    x2 += (double)xn * (double)xn;
-                }
                 a.photo_norm[2 * (size_t)photo] = g2;
                 a.photo_norm[2 * (size_t)photo + 1] = x2;
                 P.nrm[0] = g2;
                 P.nrm[1] = x2;
             }
         } else if (lane < 6) {
-            P.xp[lane] = xg[lane];
-        } else if (lane < 8) {
-            P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // written by a k_backsub flush
+            P.xp[lane] = xov;
         }
+        STAMP(18);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
             const double om1[3] = {P.xp[0], P.xp[1], P.xp[2]};
@@ -590,39 +868,39 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 9; ++k) { P.R1[k] = r1.R[k]; P.Jr1[k] = J[k]; }
         }
+        STAMP(19);
     }
     __syncthreads();
     STAMP(1);
 
-    // ---- phase A: edge prologues, one lane per edge
-    for (int le = tid; le < ne; le += blockDim.x) edge_prologue<MODEL>(a, P, ctab, e0 + le, el[le]);
-    __syncthreads();
-    STAMP(2);
 
     // ---- phase B/C: corner sweep + reduction + chain products, one wave per edge
     for (int base = 0; base < ne; base += 4) {
         const int le = base + wave;
         if (le < ne) {
             EdgeLds& L = el[le];
+            // ---- phase A: the wave's edge prologue
+            edge_prologue_wave<MODEL>(P, ctab, L, lane);
+            wave_sync_lds();
+            if (base == 0) STAMP(2);
             const int cam = L.cam, off = L.off, n = L.n;
             double R[9], T[3], kd[12];
 #pragma unroll
             for (int q = 0; q < 9; ++q) R[q] = L.R[q];
 #pragma unroll
             for (int q = 0; q < 3; ++q) T[q] = L.T[q];
-            const int nd = a.nd;
+            const double* kt = ktab + kIntrStride * cam;
 #pragma unroll
-            for (int q = 0; q < 12; ++q) kd[q] = q < nd ? (double)a.D[nd * cam + q] : 0.0;
-            const float* Kc = a.K + 9 * cam;
-            const double fx = Kc[0], fy = Kc[4], cx = Kc[2], cy = Kc[5], sk = Kc[1];
-            const double xi = MODEL == MCC_MODEL_OMNI ? (double)a.xi[cam] : 0.0;
+            for (int q = 0; q < 12; ++q) kd[q] = kt[6 + q];
+            const double fx = kt[0], fy = kt[1], cx = kt[2], cy = kt[3], sk = kt[4];
+            const double xi = kt[5];
             double acc[32];
 #pragma unroll
             for (int q = 0; q < 32; ++q) acc[q] = 0.0;
             for (int i = lane; i < n; i += 64) {
-                const int c = off + i;
-                const double X = a.obj_x[c], Y = a.obj_y[c], Z = a.obj_z[c];
-                const float ou = a.img_u[c], ov = a.img_v[c];
+                const int c = off + i;   // photo-local corner (staged in LDS)
+                const double X = cs[c], Y = cs[a.max_cpp + c], Z = cs[2 * a.max_cpp + c];
+                const float ou = cs[3 * a.max_cpp + c], ov = cs[4 * a.max_cpp + c];
                 double Yr[3], D[6];
                 float u, v;
                 if (MODEL == MCC_MODEL_OMNI)
@@ -630,7 +908,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 else
                     pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
                 const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
-                if (a.resid) { a.resid[2 * c] = euf; a.resid[2 * c + 1] = evf; }
+                if (a.resid) { a.resid[2 * ((size_t)c0 + c)] = euf; a.resid[2 * ((size_t)c0 + c) + 1] = evf; }
                 const double eu = euf, ev = evf;
                 double ju[6], jv[6];   // J' rows: [Y x d, d]
                 ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
@@ -664,7 +942,10 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 }
             }
         }
-        __syncthreads();
+        // each wave owns its edge: wave-local ordering of the LDS records is enough
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         STAMP(4);
         if (le < ne) {   // X = A' G  (A' symmetric)
             EdgeLds& L = el[le];
@@ -677,7 +958,9 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 (w ? L.Xg : L.Xp)[ij] = s;
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (le < ne) {   // H = G^T X, g = G^T b'
             EdgeLds& L = el[le];
             for (int t = lane; t < 120; t += 64) {
@@ -699,8 +982,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 }
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
 
     // ---- phase D: photo block: Hpp = sum_e, Cholesky, z = L^-1 gp, Y_e = Hgp_e L^-T
     STAMP(5);
@@ -800,6 +1083,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         const EdgeLds& L = el[tid];
         P.eg[tid] = L.has_global ? (MODEL == MCC_MODEL_DOUBLESIDE ? 0 : L.cam - 1) : -1;
     }
+    __syncthreads();
+    if (tid < 5) {   // per camera block (m <= 30: at most 5) the photo's edges in edge order
+        int cnt = 0;
+        for (int e = 0; e < ne; ++e)
+            if (P.eg[e] == tid) P.bl[tid][min(cnt++, 63)] = e;
+        P.bn[tid] = min(cnt, 64);
+    }
     // ---- phase E (fused step, m <= 30): this photo's packed contribution
     //   S[i][j] (i <= j) = sum_{a: g_a = i/6} sum_{b: g_b = j/6} ([a == b] Hgg_a - Y_a Y_b^T)[i%6][j%6]
     //   r[i] = sum_{a: g_a = i/6} (gg_a - Y_a z)[i%6],  jte_g[i] = sum gg_a[i%6],  norms of the update
@@ -814,11 +1104,12 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             int i, j;
             packed_ij(t, m, i, j);
             const int bi = i / 6, bj = j / 6, ii = i % 6, jj = j % 6;
-            for (int ea = 0; ea < ne; ++ea) {
-                if (P.eg[ea] != bi) continue;
+            const int na = P.bn[bi], nb2 = P.bn[bj];
+            for (int qa = 0; qa < na; ++qa) {
+                const int ea = P.bl[bi][qa];
                 const EdgeLds& La = el[ea];
-                for (int eb = 0; eb < ne; ++eb) {
-                    if (P.eg[eb] != bj) continue;
+                for (int qb = 0; qb < nb2; ++qb) {
+                    const int eb = P.bl[bj][qb];
                     const EdgeLds& Lb = el[eb];
                     double d = 0.0;
 #pragma unroll
@@ -829,9 +1120,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             }
         } else if (t < ntri + 2 * m) {
             const int u = t - ntri, w = u / m, i = u % m, bi = i / 6, ii = i % 6;
-            for (int ea = 0; ea < ne; ++ea) {
-                if (P.eg[ea] != bi) continue;
-                const EdgeLds& La = el[ea];
+            for (int qa = 0; qa < P.bn[bi]; ++qa) {
+                const EdgeLds& La = el[P.bl[bi][qa]];
                 if (w == 0) {
                     double d = 0.0;
 #pragma unroll
@@ -888,7 +1178,11 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     if (!a.fuse_solve) { RSTAMP(15); return; }
     __syncthreads();
     STAMP(12);
-    solve_global(a.solve, S, rr, nrm2[0], nrm2[1]);
+    SolveCtx sc = a.solve;
+#ifdef MCC_DIAG
+    sc.stamps = a.stamps ? a.stamps + kStampStride * (size_t)photo + 20 : nullptr;   // slots 20..26
+#endif
+    solve_global(sc, S, rr, nrm2[0], nrm2[1]);
     STAMP(13);
     RSTAMP(15);
 }
@@ -905,12 +1199,6 @@ __device__ __forceinline__ double sub_sum(double v, int tpr) {
 // lane i owns row i.  Step k broadcasts only row k right of the pivot (m - k values, v_readlane
 // with a compile-time lane) -- about m^2/2 broadcasts in all -- and every lane i != k eliminates
 // its column-k entry.  S is SPD: no pivoting.  Writes delta_i = r_i / S_ii into r[].
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const unsigned long long b = __double_as_longlong(v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
-    return __longlong_as_double(((unsigned long long)hi << 32) | lo);
-}
 
 template <int MM>
 __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int lane, int* err) {
@@ -926,7 +1214,9 @@ __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int l
         if (k >= m) break;
         const double piv = readlane_f64(row[k], k);
         bad |= !(piv > 0.0);
-        const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
+        const double pv = piv > 0.0 ? piv : 1.0;
+        double ip = __builtin_amdgcn_rcp(pv);   // v_rcp_f64 (~2^-26 rel), one Newton step -> ~1 ulp
+        ip = fma(ip, fma(-pv, ip, 1.0), ip);
         if (lane == k) dii = piv;
         const double f = lane == k ? 0.0 : row[k] * ip;
 #pragma unroll
@@ -954,6 +1244,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     const int m = a.m, tid = threadIdx.x;
     __shared__ int stop;
     __shared__ double s_alpha;
+    SSTAMP(a.stamps, 0, 0);
     if (tid == 0) {
         const int k = st->iter;
         double change = 1.0;
@@ -974,11 +1265,13 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     } else if (m <= 30 && tid >= 64 && tid < 128) {
         // speculative: the elimination does not depend on the stop test (its result is unused
         // when the loop stops), so wave 1 runs it while wave 0 loads the state
+        SSTAMP(a.stamps, 1, 64);
         gj_dispatch(S, r, m, tid - 64, &st->error);
+        SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();
     if (stop) return;
-    STAMPP(a.stamps, 8, 4);
+    SSTAMP(a.stamps, 4, 0);
     if (m > 30) {
         // ---- Gauss-Jordan elimination of [S | r] without row scaling (S is SPD: no pivoting).
         // Step k updates rows i != k, columns j > k and r from the (unchanged) pivot row/column, so
@@ -1005,7 +1298,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         for (int i = tid; i < m; i += blockDim.x) r[i] = r[i] / S[i * m + i];
         __syncthreads();
     }
-    STAMPP(a.stamps, 8, 5);
+    SSTAMP(a.stamps, 5, 0);
     if (tid < 64) {
         const int lane = tid;
         // global block: delta, update, norm partials (identical on every rank)
@@ -1023,7 +1316,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
                 x2 += (double)xn * (double)xn;
             }
         }
-        STAMPP(a.stamps, 8, 6);
+        SSTAMP(a.stamps, 6, 0);
         g2 = wave_sum(g2);
         x2 = wave_sum(x2);
         if (lane == 0 && a.do_update) {
@@ -1175,7 +1468,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     __syncthreads();
     STAMPP(a.stamps, 8, 3);
     SolveCtx sc = a.solve;
-    sc.stamps = a.stamps;
+    sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
     solve_global(sc, S, r, norms[0], norms[1]);
     STAMPP(a.stamps, 8, 7);
 }
@@ -1362,15 +1655,17 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     return hipGetLastError();
 }
 
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused) {
-    const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) + 18 * sizeof(double) * (size_t)n_cams;
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp) {
+    const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
+                       (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
+                       ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15);
     return fused ? std::max(lin, (size_t)(m * m + m) * sizeof(double)) : lin;
 }
 
 size_t mcc_solve_shmem(int m) { return (size_t)(m * m + m) * sizeof(double); }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused);
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
         case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
@@ -1378,9 +1673,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused) {
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp) {
     hipError_t err = hipSuccess;
-    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused);
+    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused, max_cpp);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
         for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),

@@ -7,7 +7,8 @@ run time: read its shares.
 
 Slots per workgroup (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written,
 9 group ticket won, 10 group sum written, 11 final ticket won, 12 system assembled, 13 solved
-(fused step); 14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit.  s_memtime is per XCD,
+(fused step); 14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit; 16, 18, 19 phase-0 detail
+(loads, back-solve, photo Rodrigues).  s_memtime is per XCD,
 so only differences within one workgroup are meaningful; the cross-workgroup timeline uses 14/15.
 """
 import os
@@ -38,14 +39,16 @@ def main():
     ba.synchronize()
     raw = ba.stamps().reshape(-1)
     nv = max(p.n_photos, 1)
-    s = raw[:16 * nv].reshape(nv, 16).astype(np.float64)
-    sch = raw[16 * nv:].reshape(-1, 8).astype(np.float64)
+    s = raw[:32 * nv].reshape(nv, 32).astype(np.float64)
+    sch = raw[32 * nv:].reshape(-1, 8).astype(np.float64)
     s = s[s[:, 0] > 0]
     d = np.diff(s[:, :8], axis=1)
     print(f"{cfg}: {len(s)} workgroups stamped (s_memtime ticks)")
     for k, name in enumerate(PHASES):
         print(f"  {name:16s} {med(d[:, k])}")
     print(f"  {'linearize total':16s} {med(s[:, 7] - s[:, 0])}")
+    print(f"  phase 0: loads+partials {med(s[:, 16] - s[:, 0])}; back-solve/update {med(s[:, 18] - s[:, 16])}; "
+          f"photo Rodrigues {med(s[:, 19] - s[:, 18])}; barrier {med(s[:, 1] - s[:, 19])}")
     fused = (s[:, 8] > 0).any()
     if fused:
         print(f"  {'contribution':16s} {med(s[:, 8] - s[:, 7])}")
@@ -55,6 +58,9 @@ def main():
         if len(f):
             F = f[0]
             print(f"  final: ticket {F[11] - F[10]:.0f}, assemble {F[12] - F[11]:.0f}, solve {F[13] - F[12]:.0f}")
+            sv = F[20:27]
+            print(f"  solve: stop test (wave 0) {sv[4] - sv[0]:.0f} incl. barrier; GJ (wave 1) {sv[2] - sv[1]:.0f}; "
+                  f"after GJ -> update start {sv[5] - sv[4]:.0f}; update {sv[6] - sv[5]:.0f}; tail {F[13] - sv[6]:.0f}")
     r0, r1 = s[:, 14], s[:, 15]
     ok = r1 > 0
     if ok.any():
