@@ -75,13 +75,67 @@ __device__ __forceinline__ void bfly_step(double* v, int lane) {
         v[j] = keep + __shfl_xor(send, 2 * W);
     }
 }
+// Cross-lane exchanges in VALU (no LDS crossbar): v_permlane32_swap / v_permlane16_swap
+// (gfx950) move whole half-waves / rows, DPP row_ror / quad_perm the rest.
+__device__ __forceinline__ double ull_f64(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// vdst = a, src = b: lanes 32-63 of a <-> lanes 0-31 of b
+__device__ __forceinline__ void pl32_swap(double& a, double& b) {
+    const unsigned long long A = __double_as_longlong(a), B = __double_as_longlong(b);
+    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)A, (unsigned)B, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(A >> 32), (unsigned)(B >> 32), false, false);
+    a = ull_f64(l[0], h[0]);
+    b = ull_f64(l[1], h[1]);
+}
+// odd rows (16 lanes) of a <-> even rows of b
+__device__ __forceinline__ void pl16_swap(double& a, double& b) {
+    const unsigned long long A = __double_as_longlong(a), B = __double_as_longlong(b);
+    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)A, (unsigned)B, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(A >> 32), (unsigned)(B >> 32), false, false);
+    a = ull_f64(l[0], h[0]);
+    b = ull_f64(l[1], h[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return ull_f64((unsigned)lo, (unsigned)hi);
+}
+constexpr int kDppRor4 = 0x124, kDppRor8 = 0x128, kDppRor12 = 0x12C;   // row_ror:n, dst[i] = src[(i - n) & 15]
+constexpr int kDppXor2 = 0x4E, kDppXor1 = 0xB1;                         // quad_perm [2,3,0,1] / [1,0,3,2]
+
+// Same butterfly as bfly_step<16..1> + final xor 1 (lanes with the partner bit set keep the
+// upper half), with every exchange in VALU.
 __device__ __forceinline__ double wave_reduce_scatter32(double* v, int lane) {
-    bfly_step<16>(v, lane);
-    bfly_step<8>(v, lane);
-    bfly_step<4>(v, lane);
-    bfly_step<2>(v, lane);
-    bfly_step<1>(v, lane);
-    return v[0] + __shfl_xor(v[0], 1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { double a = v[j], b = v[j + 16]; pl32_swap(a, b); v[j] = a + b; }   // xor 32
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { double a = v[j], b = v[j + 8]; pl16_swap(a, b); v[j] = a + b; }      // xor 16
+    {
+        const bool hi = (lane & 8) != 0;   // xor 8: rotate a row by 8
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double send = hi ? v[j] : v[j + 4], keep = hi ? v[j + 4] : v[j];
+            v[j] = keep + dpp_f64<kDppRor8>(send);
+        }
+    }
+    {
+        const bool hi = (lane & 4) != 0;   // xor 4: i - 4 for the upper, i + 4 = i - 12 for the lower
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const double send = hi ? v[j] : v[j + 2], keep = hi ? v[j + 2] : v[j];
+            const double p4 = dpp_f64<kDppRor4>(send), p12 = dpp_f64<kDppRor12>(send);
+            v[j] = keep + (hi ? p4 : p12);
+        }
+    }
+    {
+        const bool hi = (lane & 2) != 0;   // xor 2
+        const double send = hi ? v[0] : v[1], keep = hi ? v[1] : v[0];
+        v[0] = keep + dpp_f64<kDppXor2>(send);
+    }
+    return v[0] + dpp_f64<kDppXor1>(v[0]);   // xor 1
 }
 __device__ __forceinline__ int bfly_index(int lane) {
     return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
@@ -1219,12 +1273,19 @@ __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int l
         ip = fma(ip, fma(-pv, ip, 1.0), ip);
         if (lane == k) dii = piv;
         const double f = lane == k ? 0.0 : row[k] * ip;
+        // broadcast the whole pivot row first (distinct SGPR pairs, back-to-back v_readlane),
+        // then the updates: no readlane -> use -> readlane reuse of one SGPR pair per column
+        double pr[MM + 1];
+#pragma unroll
+        for (int j = k + 1; j < MM; ++j) pr[j] = j < m ? readlane_f64(row[j], k) : 0.0;
+        pr[MM] = readlane_f64(rr, k);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = k + 1; j < MM; ++j) {
             if (j >= m) break;
-            row[j] -= f * readlane_f64(row[j], k);
+            row[j] -= f * pr[j];
         }
-        rr -= f * readlane_f64(rr, k);
+        rr -= f * pr[MM];
     }
     if (bad && lane == 0) atomicOr(err, 2);
     if (lane < m) r[lane] = rr / dii;
