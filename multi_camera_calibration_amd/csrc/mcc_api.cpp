@@ -123,7 +123,7 @@ struct mcc_problem {
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
-    DevBuf<double> ds_rt, Y, Hgg, gg, Lp, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum;
+    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum;
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
@@ -169,7 +169,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.cam_rt = p->cam_rt.p; la.ds_rt = p->ds_rt.p;
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
-    la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.gg = p->gg.p; la.Lp = p->Lp.p; la.zp = p->zp.p;
+    la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.Hgp = p->Hgp.p; la.gg = p->gg.p; la.zp = p->zp.p;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
     la.gblock = p->edge_gblock.p;
@@ -205,7 +205,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     SchurArgs sa{};
     sa.state = p->state.p;
     sa.items = p->items.p; sa.pairs = p->pairs.p;
-    sa.Y = p->Y.p; sa.Hgg = p->Hgg.p; sa.gg = p->gg.p; sa.zp = p->zp.p;
+    sa.Y = p->Y.p; sa.Hgg = p->Hgg.p; sa.Hgp = p->Hgp.p; sa.gg = p->gg.p; sa.gp_tot = p->gp_tot.p;
     sa.item_out = p->item_out.p;
     sa.n_items = p->n_items;
     sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
@@ -233,7 +233,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
 // standalone photo back-substitution: deltaX of the photos (do_update = 0) or a flush of the
 // pending update (do_update = 1)
 int enqueue_backsub(mcc_problem* p, int do_update) {
-    mcc::BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->Lp.p, p->zp.p, p->dg.p,
+    mcc::BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->zp.p, p->dg.p,
                         p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
     HIPCHK(mcc_launch_backsub(ba, p->stream));
     return MCC_OK;
@@ -504,7 +504,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E)); HIPC(p->Hgg.alloc(36 * (size_t)E)); HIPC(p->gg.alloc(6 * (size_t)E));
-    HIPC(p->Lp.alloc(42 * (size_t)V));   // L + 1/L_ii per photo
+    HIPC(p->Hgp.alloc(36 * (size_t)E));
     HIPC(p->zp.alloc(6 * (size_t)V));
     HIPC(p->gp_tot.alloc(6 * (size_t)V));
     // + 24 zeroed items of padding: the assembly loads a fixed 24 items per block unconditionally
@@ -553,7 +553,7 @@ void mcc_destroy(mcc_problem* p) {
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release();
-    p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Lp.release(); p->zp.release();
+    p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Hgp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release();

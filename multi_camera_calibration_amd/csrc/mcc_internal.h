@@ -47,11 +47,11 @@ struct LinArgs {
     const double* ds_rt;      // PINHOLE doubleSideTransform (rvec, tvec) [6]
     int nd, global_dim, n_cams, has_back;
     // outputs
-    double* Y;        // [36E] Schur factors Hgp_e L_p^-T
-    double* Hgg;      // [36E]
-    double* gg;       // [6E]
-    double* Lp;       // [42V] L (6x6 lower) + 1/L_ii
-    double* zp;       // [6V]
+    double* Y;        // [36E] Schur factors Y'_e = Hgp_e Hpp^-1
+    double* Hgg;      // [36E] (k_schur path)
+    double* Hgp;      // [36E] (k_schur path)
+    double* gg;       // [6E] (k_schur path)
+    double* zp;       // [6V] z' = Hpp^-1 gp
     double* gp_tot;   // [6V] photo JTE
     float* resid;     // optional [2*corners] float32 residuals (debug)
     // pending update of the previous step (fused back-substitution)
@@ -75,7 +75,7 @@ struct SchurArgs {
     State* state;
     const int4* items;   // {block, pair_begin, pair_end, -}
     const int4* pairs;   // {e1, e2, photo, self}
-    const double* Y; const double* Hgg; const double* gg; const double* zp;
+    const double* Y; const double* Hgg; const double* Hgp; const double* gg; const double* gp_tot;
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;
     const double* photo_norm; int n_photos;
@@ -96,7 +96,7 @@ struct BacksubArgs {
     const State* state;
     const int* photo_ptr;
     const int* gblock;
-    const double* Y; const double* Lp; const double* zp; const double* dg;
+    const double* Y; const double* zp; const double* dg;
     float* x;
     double* delta;
     double* photo_norm;

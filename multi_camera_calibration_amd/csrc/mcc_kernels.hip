@@ -155,7 +155,6 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-constexpr int kLpStride = 42;   // per photo: L (6x6, lower) + 1/L_ii
 constexpr int kCamStride = 24;  // LDS camera table row: R (9), Jl (9), T (3), pad
 constexpr int kIntrStride = 20; // LDS intrinsics row: fx, fy, cx, cy, skew, xi, k[12], pad
 
@@ -202,7 +201,8 @@ struct PhotoLds {
     double Hs[36], gs[6], Lm[36], z[6], il[6];
     double dgl[128];     // global-block delta of the previous solve (pending update)
     double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
-    int eg[64];          // global block of each edge of the photo or -1 (fused step)
+    double cn[2];        // state snapshot: camera-block ||G||^2, ||x||^2 of the last update
+    int iter0, pad1[3];  // state snapshot: completed updates
     int bn[8];           // per camera block: number of the photo's edges in it (fused step)
     unsigned char bl[5][64];   // per camera block: those edges in edge order
     // followed by the camera table [C][kCamStride], the intrinsics [C][kIntrStride] and the
@@ -653,10 +653,10 @@ __device__ __forceinline__ void omni_corner(const double* R, const double* T, co
 }
 
 // ---------------------------------------------------------------- photo back-substitution
-// dp = L^-T (z - sum_e Y_e^T dg_e) for one photo (one thread); used by k_backsub.
+// dp = z - sum_e Y_e^T dg_e (z = Hpp^-1 gp, Y_e = Hgp_e Hpp^-1) for one photo (one thread);
+// used by k_backsub.
 __device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gblock, const double* Y,
-                                           const double* Lp, const double* zp, const double* dg, int p,
-                                           double t[6]) {
+                                           const double* zp, const double* dg, int p, double t[6]) {
     const double* z = zp + 6 * (size_t)p;
 #pragma unroll
     for (int k = 0; k < 6; ++k) t[k] = z[k];
@@ -672,14 +672,6 @@ __device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gbl
             for (int i = 0; i < 6; ++i) s += Ye[i * 6 + k] * d[i];
             t[k] -= s;
         }
-    }
-    const double* Lm = Lp + kLpStride * (size_t)p;
-#pragma unroll
-    for (int i = 5; i >= 0; --i) {
-        double s = t[i];
-#pragma unroll
-        for (int k = i + 1; k < 6; ++k) s -= Lm[k * 6 + i] * t[k];
-        t[i] = s * Lm[36 + i];
     }
 }
 
@@ -792,17 +784,33 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     if (wave == 0) {
         if (lane < 6) xov = xg[lane];
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
+        else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
+        else if (lane == 10) P.iter0 = st->iter;
         if (pending) {
-            if (lane < 42) lov = a.Lp[kLpStride * (size_t)photo + lane];   // L (36) + 1/L_ii (6)
-            else if (lane < 48) lov = a.zp[6 * (size_t)photo + lane - 42];
+            if (lane >= 42 && lane < 48) lov = a.zp[6 * (size_t)photo + lane - 42];   // z' = Hpp^-1 gp
+            // lane l < 60: k = l % 6, edges l / 6, l / 6 + 10, ...: sum_i Y_e[i][k] dg_{g(e)}[i].
+            // The first edge's Y column and block are loaded before dg is staged, so the two
+            // global round trips overlap.
+            const int k = lane % 6, le0 = lane / 6;
+            const bool has0 = lane < 60 && le0 < ne;
+            double y0[6];
+            int g0 = -1;
+            if (has0) {
+                g0 = a.gblock[e0 + le0];
+                const double* Ye = a.Y + 36 * (size_t)(e0 + le0) + k;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y0[i] = Ye[6 * i];
+            }
             for (int q = lane; q < a.global_dim; q += 64) P.dgl[q] = a.dg[q];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // lane l < 60: k = l % 6, edges l / 6, l / 6 + 10, ...: sum_i Y_e[i][k] dg_{g(e)}[i]
+            if (has0 && g0 >= 0) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) part += y0[i] * P.dgl[6 * g0 + i];
+            }
             if (lane < 60) {
-                const int k = lane % 6;
-                for (int le = lane / 6; le < ne; le += 10) {
+                for (int le = le0 + 10; le < ne; le += 10) {
                     const int g = a.gblock[e0 + le];
                     if (g < 0) continue;
                     const double* Ye = a.Y + 36 * (size_t)(e0 + le) + k;
@@ -858,6 +866,12 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             for (int k = 0; k < 9; ++k) { P.Rds[k] = rd.R[k]; P.Jrds[k] = J[k]; }
         }
     } else {
+        // wave 2 lanes < ne: the edge records (off wave 0's pending-update path)
+        for (int le = tid - 128; le < ne; le += 64) {
+            const int4 info = a.edge_info[e0 + le];
+            EdgeLds& L = el[le];
+            L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
+        }
         // the photo's corners are contiguous (photo-major layout): stage all five streams
         for (int q = tid - 128; q < ncs; q += 128) {
             const size_t c = (size_t)c0 + q;
@@ -868,15 +882,10 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             cs[4 * a.max_cpp + q] = a.img_v[c];
         }
     }
-    for (int le = tid; le < ne; le += blockDim.x) {
-        const int4 info = a.edge_info[e0 + le];
-        EdgeLds& L = el[le];
-        L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
-    }
     STAMP(16);
     if (wave == 0) {
         if (pending) {
-            // fused back-substitution of the previous step: dp = L^-T (z - sum_e Y_e^T dg_e),
+            // fused back-substitution of the previous step: dp = z' - sum_e Y_e^T dg_e,
             // operands gathered from wave 0's registers with compile-time v_readlane
             double t[6];
 #pragma unroll
@@ -885,13 +894,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
                 for (int j = 0; j < 10; ++j) sacc -= readlane_f64(part, 6 * j + q);
                 t[q] = sacc;
-            }
-#pragma unroll
-            for (int i = 5; i >= 0; --i) {
-                double sacc = t[i];
-#pragma unroll
-                for (int q = i + 1; q < 6; ++q) sacc -= readlane_f64(lov, q * 6 + i) * t[q];
-                t[i] = sacc * readlane_f64(lov, 36 + i);
             }
             double g2 = 0.0, x2 = 0.0;
 #pragma unroll
@@ -1039,89 +1041,82 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     }
     __syncthreads();
 
-    // ---- phase D: photo block: Hpp = sum_e, Cholesky, z = L^-1 gp, Y_e = Hgp_e L^-T
+    // ---- phase D: photo block Hpp = sum_e Hpp_e, its inverse (register Gauss-Jordan on wave 0,
+    // Hpp is SPD), z' = Hpp^-1 gp and the Schur factors Y'_e = Hgp_e Hpp^-1: the reduced camera
+    // system is S = sum (Hgg - Y'_a Hgp_b^T), r = sum (gg - Y'_a gp), and the photo step of a
+    // global step dg is dp = z' - sum_e Y'_e^T dg_e (no triangular solves anywhere)
     STAMP(5);
-    double* Hs = P.Hs;
     double* gs = P.gs;
-    double* Lm = P.Lm;
+    double* Hi = P.Lm;   // Hpp^-1
     double* z = P.z;
-    if (tid < 42) {
-        double sacc = 0.0;
-        for (int le = 0; le < ne; ++le) sacc += tid < 36 ? el[le].Hpp[tid] : el[le].gp[tid - 36];
-        if (tid < 36) Hs[tid] = sacc; else gs[tid - 36] = sacc;
-    }
-    __syncthreads();
-    if (tid == 0) {   // register-resident 6x6 Cholesky (packed lower, in place) + forward substitution
-        double Lr[21], il[6], zz[6];
+    if (wave == 0) {
+        // lane i < 6 owns row i of [Hpp | I] (summed over the photo's edges in edge order);
+        // lanes >= 6 sum row 0 and stay idle; lanes 6..11 also sum gp
+        const int li = lane < 6 ? lane : 0;
+        double row[12];
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) { row[j] = 0.0; row[6 + j] = li == j ? 1.0 : 0.0; }
+        double gsum = 0.0;
+        for (int le = 0; le < ne; ++le) {
 #pragma unroll
-            for (int j = 0; j <= i; ++j) Lr[i * (i + 1) / 2 + j] = Hs[i * 6 + j];
-        int ok = 1;
+            for (int j = 0; j < 6; ++j) row[j] += el[le].Hpp[li * 6 + j];
+            if (lane >= 6 && lane < 12) gsum += el[le].gp[lane - 6];
+        }
+        if (lane >= 6 && lane < 12) gs[lane - 6] = gsum;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double dii = 1.0;
+        bool bad = false;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            double sacc = Lr[j * (j + 1) / 2 + j];
+        for (int k = 0; k < 6; ++k) {
+            const double piv = readlane_f64(row[k], k);
+            bad |= !(piv > 0.0);
+            const double pv = piv > 0.0 ? piv : 1.0;
+            double ip = __builtin_amdgcn_rcp(pv);
+            ip = fma(ip, fma(-pv, ip, 1.0), ip);
+            if (lane == k) dii = pv;
+            const double f = lane == k ? 0.0 : row[k] * ip;
+            double pr[12];
 #pragma unroll
-            for (int q = 0; q < j; ++q) sacc -= Lr[j * (j + 1) / 2 + q] * Lr[j * (j + 1) / 2 + q];
-            if (!(sacc > 0.0)) { ok = 0; sacc = 1.0; }
-            const double l = sqrt(sacc);
-            il[j] = 1.0 / l;
-            Lr[j * (j + 1) / 2 + j] = l;
+            for (int j = k + 1; j < 12; ++j) pr[j] = readlane_f64(row[j], k);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = j + 1; i < 6; ++i) {
-                double t = Lr[i * (i + 1) / 2 + j];
+            for (int j = k + 1; j < 12; ++j) row[j] -= f * pr[j];
+        }
+        if (lane < 6) {
+            const double id = 1.0 / dii;
+            double zi = 0.0;
 #pragma unroll
-                for (int q = 0; q < j; ++q) t -= Lr[i * (i + 1) / 2 + q] * Lr[j * (j + 1) / 2 + q];
-                Lr[i * (i + 1) / 2 + j] = t * il[j];
+            for (int j = 0; j < 6; ++j) {
+                const double h = row[6 + j] * id;
+                Hi[lane * 6 + j] = h;
+                zi += h * gs[j];
             }
+            z[lane] = zi;
         }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            double sacc = gs[i];
-#pragma unroll
-            for (int q = 0; q < i; ++q) sacc -= Lr[i * (i + 1) / 2 + q] * zz[q];
-            zz[i] = sacc * il[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            z[i] = zz[i];
-            P.il[i] = il[i];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) Lm[i * 6 + j] = j <= i ? Lr[i * (i + 1) / 2 + j] : 0.0;
-        }
-        if (!ok) atomicOr(&st->error, 1);
+        if (bad && lane == 0) atomicOr(&st->error, 1);
     }
     __syncthreads();
     STAMP(6);
-    if (tid < 36) a.Lp[kLpStride * (size_t)photo + tid] = Lm[tid];
-    else if (tid >= 48 && tid < 54) a.Lp[kLpStride * (size_t)photo + 36 + tid - 48] = P.il[tid - 48];
-    else if (tid < 42) a.zp[6 * (size_t)photo + tid - 36] = z[tid - 36];
-    else if (tid < 48) a.gp_tot[6 * (size_t)photo + tid - 42] = gs[tid - 42];
-    for (int t = tid; t < 6 * ne; t += blockDim.x) {
-        const int le = t / 6, i = t % 6;
+    if (tid >= 36 && tid < 42) a.zp[6 * (size_t)photo + tid - 36] = z[tid - 36];
+    else if (tid >= 42 && tid < 48) a.gp_tot[6 * (size_t)photo + tid - 42] = gs[tid - 42];
+    for (int t = tid; t < 36 * ne; t += blockDim.x) {
+        const int le = t / 36, ij = t % 36, i = ij / 6, j = ij % 6;
         EdgeLds& L = el[le];
-        const int e = e0 + le;
-        double y[6];
+        const size_t e = (size_t)(e0 + le);
+        double y = 0.0;
         if (L.has_global) {
-            for (int j = 0; j < 6; ++j) {
-                double s = L.Hgp[i * 6 + j];
-                for (int k = 0; k < j; ++k) s -= Lm[j * 6 + k] * y[k];
-                y[j] = s * P.il[j];
-            }
-        } else {
-            for (int j = 0; j < 6; ++j) y[j] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) y += L.Hgp[i * 6 + k] * Hi[k * 6 + j];
         }
-        double* Yo = a.Y + 36 * (size_t)e + 6 * i;
+        a.Y[36 * e + ij] = y;
         if (a.fused) {
-            // Xg (A' Gg scratch) is dead: it holds row i of Y_e for the contribution below
-            for (int j = 0; j < 6; ++j) { Yo[j] = y[j]; L.Xg[i * 6 + j] = y[j]; }
+            L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the contribution below
         } else {
-            double* Ho = a.Hgg + 36 * (size_t)e + 6 * i;
-            for (int j = 0; j < 6; ++j) {
-                Yo[j] = y[j];
-                Ho[j] = L.has_global ? L.Hgg[i * 6 + j] : 0.0;
-            }
-            a.gg[6 * (size_t)e + i] = L.has_global ? L.gg[i] : 0.0;
+            a.Hgg[36 * e + ij] = L.has_global ? L.Hgg[ij] : 0.0;
+            a.Hgp[36 * e + ij] = L.has_global ? L.Hgp[ij] : 0.0;
+            if (j == 0) a.gg[6 * e + i] = L.has_global ? L.gg[i] : 0.0;
         }
     }
     if (!a.fused) {
@@ -1133,16 +1128,15 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         return;
     }
 
-    if (tid < ne) {
-        const EdgeLds& L = el[tid];
-        P.eg[tid] = L.has_global ? (MODEL == MCC_MODEL_DOUBLESIDE ? 0 : L.cam - 1) : -1;
-    }
-    __syncthreads();
-    if (tid < 5) {   // per camera block (m <= 30: at most 5) the photo's edges in edge order
+    if (tid >= 192 && tid < 197) {   // per camera block (m <= 30: at most 5) the photo's edges in edge order
+        const int b = tid - 192;
         int cnt = 0;
-        for (int e = 0; e < ne; ++e)
-            if (P.eg[e] == tid) P.bl[tid][min(cnt++, 63)] = e;
-        P.bn[tid] = min(cnt, 64);
+        for (int e = 0; e < ne; ++e) {
+            const EdgeLds& L = el[e];
+            const int g = L.has_global ? (MODEL == MCC_MODEL_DOUBLESIDE ? 0 : L.cam - 1) : -1;
+            if (g == b) P.bl[b][min(cnt++, 63)] = e;
+        }
+        P.bn[b] = min(cnt, 64);
     }
     // ---- phase E (fused step, m <= 30): this photo's packed contribution
     //   S[i][j] (i <= j) = sum_{a: g_a = i/6} sum_{b: g_b = j/6} ([a == b] Hgg_a - Y_a Y_b^T)[i%6][j%6]
@@ -1167,7 +1161,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                     const EdgeLds& Lb = el[eb];
                     double d = 0.0;
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * Lb.Xg[jj * 6 + k];
+                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * Lb.Hgp[jj * 6 + k];
                     v -= d;
                     if (ea == eb) v += La.Hgg[ii * 6 + jj];
                 }
@@ -1179,7 +1173,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 if (w == 0) {
                     double d = 0.0;
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * z[k];
+                    for (int k = 0; k < 6; ++k) d += La.Xg[ii * 6 + k] * gs[k];
                     v += La.gg[ii] - d;
                 } else {
                     v += La.gg[ii];
@@ -1208,6 +1202,9 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     double* S = smem;            // the edge records are dead: m*m + m doubles for the solve
     double* rr = smem + m * m;
     __shared__ double nrm2[2];
+    const int iter0 = P.iter0;   // read before S overwrites the photo record
+    const double cnG = P.cn[0], cnX = P.cn[1];
+    __syncthreads();
     for (int t = tid; t < Lc; t += blockDim.x) {
         double v = 0.0;
         v = sum_sc1(a.gsum + t, a.n_groups, Lc);
@@ -1220,8 +1217,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             rr[t - ntri] = v;
         } else if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
             const int w = t - ntri - 2 * m;
-            if (st->iter > 0) {
-                if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
+            if (iter0 > 0) {
+                if (a.rank == 0) v += w ? cnX : cnG;
             } else {
                 v = 0.0;
             }
@@ -1390,7 +1387,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 }
 
 // ---------------------------------------------------------------- k_schur
-// Work item: pairs [begin, end) of one camera-pair block.  Thread t < 240: entry q = t % 48
+// Work item: pairs [begin, end) of one camera-pair block (S_ab -= Y'_a Hgp_b^T, r_a += gg_a - Y'_a gp).  Thread t < 240: entry q = t % 48
 // (0..35: S entry, 36..41: r entry, 42..47: JTE of the global block), sub-chunk s = t / 48.
 // Norm items sum 256 photos' norm partials.  The last workgroup to finish assembles the packed
 // system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2] in fixed order, and with
@@ -1417,20 +1414,20 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
                 const double* Y1 = a.Y + 36 * (size_t)pr.x;
                 if (q < 36) {
                     const int i = q / 6, j = q % 6;
-                    const double* Y2 = a.Y + 36 * (size_t)pr.y;
+                    const double* H2 = a.Hgp + 36 * (size_t)pr.y;
                     double t = 0.0;
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * Y2[j * 6 + k];
+                    for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * H2[j * 6 + k];
                     s -= t;
                     if (pr.w) s += a.Hgg[36 * (size_t)pr.x + q];
                 } else if (pr.w) {
                     const int i = (q - 36) % 6;
                     const double gi = a.gg[6 * (size_t)pr.x + i];
                     if (q < 42) {
-                        const double* zp = a.zp + 6 * (size_t)pr.z;
+                        const double* gpt = a.gp_tot + 6 * (size_t)pr.z;
                         double t = 0.0;
 #pragma unroll
-                        for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * zp[k];
+                        for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * gpt[k];
                         s += gi - t;
                     } else {
                         s += gi;
@@ -1561,7 +1558,7 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n_photos) return;
     double t[6];
-    photo_delta(a.photo_ptr, a.gblock, a.Y, a.Lp, a.zp, a.dg, p, t);
+    photo_delta(a.photo_ptr, a.gblock, a.Y, a.zp, a.dg, p, t);
     const int col = a.m + 6 * p;
     const double alpha = a.state->alpha;
     double g2 = 0.0, x2 = 0.0;
