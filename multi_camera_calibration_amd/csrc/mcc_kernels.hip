@@ -106,6 +106,29 @@ __device__ __forceinline__ double dpp_f64(double v) {
 constexpr int kDppRor4 = 0x124, kDppRor8 = 0x128, kDppRor12 = 0x12C;   // row_ror:n, dst[i] = src[(i - n) & 15]
 constexpr int kDppXor2 = 0x4E, kDppXor1 = 0xB1;                         // quad_perm [2,3,0,1] / [1,0,3,2]
 
+// fixed-order full wave sum: xor 32, 16 by permlane swaps of v with itself, 8, 4, 2, 1 by DPP
+__device__ __forceinline__ double wave_sum(double v) {
+    {
+        double a = v, b = v;
+        pl32_swap(a, b);
+        v = a + b;
+    }
+    {
+        double a = v, b = v;
+        pl16_swap(a, b);
+        v = a + b;
+    }
+    v += dpp_f64<kDppRor8>(v);
+    {
+        const bool hi = (threadIdx.x & 4) != 0;
+        const double p4 = dpp_f64<kDppRor4>(v), p12 = dpp_f64<kDppRor12>(v);
+        v += hi ? p4 : p12;
+    }
+    v += dpp_f64<kDppXor2>(v);
+    v += dpp_f64<kDppXor1>(v);
+    return v;
+}
+
 // Same butterfly as bfly_step<16..1> + final xor 1 (lanes with the partner bit set keep the
 // upper half), with every exchange in VALU.
 __device__ __forceinline__ double wave_reduce_scatter32(double* v, int lane) {
@@ -148,12 +171,6 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
     return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-// fixed-order full wave sum (xor butterfly)
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
 
 constexpr int kCamStride = 24;  // LDS camera table row: R (9), Jl (9), T (3), pad
 constexpr int kIntrStride = 20; // LDS intrinsics row: fx, fy, cx, cy, skew, xi, k[12], pad
@@ -1300,8 +1317,9 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
     State* st = a.state;
     const int m = a.m, tid = threadIdx.x;
-    __shared__ int stop;
+    __shared__ int stop, s_iter;
     __shared__ double s_alpha;
+    __shared__ float s_x[128];
     SSTAMP(a.stamps, 0, 0);
     if (tid == 0) {
         const int k = st->iter;
@@ -1320,6 +1338,9 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         const double alpha = a.do_update ? (k < a.n_alpha ? a.alpha[k] : pow(0.95, (double)k + 1.0)) : 0.0;
         st->alpha = alpha;
         s_alpha = alpha;
+        s_iter = k;
+    } else if (tid >= 128 && tid < 128 + m) {
+        s_x[tid - 128] = a.x[tid - 128];   // global-block parameters, fetched while wave 1 eliminates
     } else if (m <= 30 && tid >= 64 && tid < 128) {
         // speculative: the elimination does not depend on the stop test (its result is unused
         // when the loop stops), so wave 1 runs it while wave 0 loads the state
@@ -1368,7 +1389,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
             a.delta[i] = d;
             if (a.do_update) {
                 const float G = (float)(alpha * d);   // G = alpha*delta -> CV_32F (:491-496)
-                const float xn = a.x[i] + G;          // x = x + G (:501)
+                const float xn = s_x[i] + G;          // x = x + G (:501)
                 a.x[i] = xn;
                 g2 += (double)G * (double)G;
                 x2 += (double)xn * (double)xn;
@@ -1380,7 +1401,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         if (lane == 0 && a.do_update) {
             st->cam_normG2 = g2;
             st->cam_normX2 = x2;
-            st->iter = st->iter + 1;
+            st->iter = s_iter + 1;
             st->pending = 1;
         }
     }
