@@ -730,10 +730,11 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 __device__ __forceinline__ double ld_sc1(const double* p) {
     return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-__device__ __forceinline__ bool arrive_last_sc1(int* counter, int expected) {
+__device__ __forceinline__ bool arrive_last_sc1(int* counter, int expected, long long* stamp = nullptr) {
     __shared__ int last_sc1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave
     __syncthreads();
+    SSTAMP(stamp, 0, 0);
     if (threadIdx.x == 0) {
         const int t = __hip_atomic_fetch_add((gi32*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_sc1 = (t == expected - 1);
@@ -1205,7 +1206,10 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     // ---- level 1: the last photo of a group sums the group in photo order
     const int G = a.group_size, grp = photo / G, g0 = grp * G;
     const int gn = min(G, (int)gridDim.x - g0);
-    if (!arrive_last_sc1(a.cnt + grp, gn)) { RSTAMP(15); return; }
+    if (!arrive_last_sc1(a.cnt + grp, gn, a.stamps ? a.stamps + kStampStride * (size_t)photo + 28 : nullptr)) {
+        RSTAMP(15);
+        return;
+    }
     STAMP(9);
     for (int t = tid; t < Lc; t += blockDim.x) {
         double v = 0.0;

@@ -53,7 +53,9 @@ def main():
     if fused:
         print(f"  {'contribution':16s} {med(s[:, 8] - s[:, 7])}")
         g = s[s[:, 9] > 0]
-        print(f"  group reducers: {len(g)}; ticket {med(g[:, 9] - g[:, 8])}; group sum {med(g[:, 10] - g[:, 9])}")
+        print(f"  group reducers: {len(g)}; ticket {med(g[:, 9] - g[:, 8])} (drain+barrier {med(g[:, 28] - g[:, 8])}); "
+              f"group sum {med(g[:, 10] - g[:, 9])}")
+        print(f"  all photos: contribution drain+barrier {med(s[:, 28] - s[:, 8])}")
         f = s[s[:, 11] > 0]
         if len(f):
             F = f[0]
