@@ -212,7 +212,9 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.counter = p->counter.p;
     sa.block_items = p->block_items.p;
     sa.packed = p->packed.p;
-    sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = multi ? 0 : 1;
+    // m > 30: the register-tiled elimination runs in its own kernel (k_solve)
+    const bool split = multi || p->m > 30;
+    sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
     sa.solve = solve_ctx(p, do_update);
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
@@ -220,6 +222,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                        p->comm, p->stream);
         if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    }
+    if (split) {
         SolveArgs so{solve_ctx(p, do_update), p->packed.p};
         HIPCHK(mcc_launch_solve(so, p->stream));
     }

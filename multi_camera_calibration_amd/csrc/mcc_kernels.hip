@@ -767,6 +767,7 @@ __device__ __forceinline__ double sum_sc1(const double* p, int n, size_t stride)
     return v;
 }
 
+template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2);
 
 // ---------------------------------------------------------------- k_linearize
@@ -1254,7 +1255,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #ifdef MCC_DIAG
     sc.stamps = a.stamps ? a.stamps + kStampStride * (size_t)photo + 20 : nullptr;   // slots 20..26
 #endif
-    solve_global(sc, S, rr, nrm2[0], nrm2[1]);
+    solve_global<false>(sc, S, rr, nrm2[0], nrm2[1]);
     STAMP(13);
     RSTAMP(15);
 }
@@ -1309,6 +1310,90 @@ __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int l
     if (lane < m) r[lane] = rr / dii;
 }
 
+
+// Gauss-Jordan of [S | r] for m > 30 (m <= 128) by the whole workgroup with the matrix in
+// registers: thread (ti, tj) of a 16 x 16 grid owns rows ti + 16 a (a < R) and columns
+// tj + 16 b (b < CC, column m = r), loaded straight from the packed upper triangle.  Pivot
+// k = 16 ka + kr is owned by register slot ka (compile-time: the ka loop is unrolled), and
+// column slots b < ka lie left of every pivot of that block (skipped at compile time).  Per
+// pivot only its column and row travel through LDS (double-buffered: one barrier per step).
+// S is SPD: no pivoting.  Writes delta_i = r_i / S_ii into r[] (LDS).
+__device__ __forceinline__ int packed_index(int i, int j, int m) {   // i <= j
+    return i * m - i * (i - 1) / 2 + (j - i);
+}
+template <int R, int CC>
+__device__ __forceinline__ void gj_tiled(const double* packed, double* r, int m, int tid, int* err) {
+    __shared__ double colb[2][128], rowb[2][136], pivs[128];
+    const int ti = tid >> 4, tj = tid & 15, ntri = m * (m + 1) / 2;
+    double A[R][CC];
+#pragma unroll
+    for (int a = 0; a < R; ++a) {
+        const int i = ti + 16 * a;
+#pragma unroll
+        for (int b = 0; b < CC; ++b) {
+            const int j = tj + 16 * b;
+            const bool ok = i < m && j <= m;
+            const int ic = ok ? i : 0, jc = ok ? j : 0;
+            const int idx = jc == m ? ntri + ic : (ic <= jc ? packed_index(ic, jc, m) : packed_index(jc, ic, m));
+            const double v = packed[idx];
+            A[a][b] = ok ? v : 0.0;
+        }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int ka = 0; ka < CC; ++ka) {
+        if (16 * ka >= m) break;
+        const int kend = min(16, m - 16 * ka);
+        for (int kr = 0; kr < kend; ++kr) {
+            const int k = 16 * ka + kr, kb = k & 1;
+            if (ka < R && tj == kr) {   // owners of column k (slot ka) publish it
+#pragma unroll
+                for (int a = 0; a < R; ++a)
+                    if (ti + 16 * a < m) colb[kb][ti + 16 * a] = A[a][ka];
+            }
+            if (ka < R && ti == kr) {   // owners of row k (slot ka) publish it
+#pragma unroll
+                for (int b = ka; b < CC; ++b)
+                    if (tj + 16 * b <= m) rowb[kb][tj + 16 * b] = A[ka][b];
+            }
+            __syncthreads();
+            const double piv = rowb[kb][k];
+            if (tid == 0) pivs[k] = piv;
+            bad |= !(piv > 0.0);
+            const double pv = piv > 0.0 ? piv : 1.0;
+            double ip = __builtin_amdgcn_rcp(pv);
+            ip = fma(ip, fma(-pv, ip, 1.0), ip);
+            double rk[CC];
+#pragma unroll
+            for (int b = ka; b < CC; ++b) {
+                const int j = tj + 16 * b;
+                rk[b] = ((b > ka || tj > kr) && j <= m) ? rowb[kb][j <= m ? j : m] : 0.0;
+            }
+#pragma unroll
+            for (int a = 0; a < R; ++a) {
+                const int i = ti + 16 * a;
+                const double f = (i < m && i != k) ? colb[kb][i < m ? i : 0] * ip : 0.0;
+#pragma unroll
+                for (int b = ka; b < CC; ++b) A[a][b] -= f * rk[b];
+            }
+        }
+    }
+    __syncthreads();
+    if (tj == (m & 15)) {
+        const int bm = m >> 4;
+#pragma unroll
+        for (int a = 0; a < R; ++a) {
+            const int i = ti + 16 * a;
+            double v = 0.0;
+#pragma unroll
+            for (int b = 0; b < CC; ++b) v = b == bm ? A[a][b] : v;
+            if (i < m) r[i] = v / pivs[i];
+        }
+    }
+    if (bad && tid == 0) atomicOr(err, 2);
+    __syncthreads();
+}
+
 __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err) {
     switch (m) {
 #define GJ(M) case M: gj_rows<M>(S, r, m, lane, err); break;
@@ -1318,6 +1403,8 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
     }
 }
 
+// LARGE: m > 30 (k_solve only: the register-tiled elimination needs the whole workgroup's registers)
+template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
     State* st = a.state;
     const int m = a.m, tid = threadIdx.x;
@@ -1345,7 +1432,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         s_iter = k;
     } else if (tid >= 128 && tid < 128 + m) {
         s_x[tid - 128] = a.x[tid - 128];   // global-block parameters, fetched while wave 1 eliminates
-    } else if (m <= 30 && tid >= 64 && tid < 128) {
+    } else if (!LARGE && tid >= 64 && tid < 128) {
         // speculative: the elimination does not depend on the stop test (its result is unused
         // when the loop stops), so wave 1 runs it while wave 0 loads the state
         SSTAMP(a.stamps, 1, 64);
@@ -1355,31 +1442,11 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     __syncthreads();
     if (stop) return;
     SSTAMP(a.stamps, 4, 0);
-    if (m > 30) {
-        // ---- Gauss-Jordan elimination of [S | r] without row scaling (S is SPD: no pivoting).
-        // Step k updates rows i != k, columns j > k and r from the (unchanged) pivot row/column, so
-        // nothing read in step k is written in step k: one barrier per step, no cross-lane
-        // reductions.  Afterwards delta_i = r_i / S_ii.
-        const int W = m + 1;   // columns k+1..m-1 plus r
-        for (int kk = 0; kk < m; ++kk) {
-            const double piv = S[kk * m + kk];
-            if (!(piv > 0.0) && tid == 0) atomicOr(&st->error, 2);
-            const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
-            const int ncol = m - kk;   // j in kk+1..m-1 (ncol-1 of them) + r
-            for (int i = tid >> 4; i < m; i += 16) {
-                if (i == kk) continue;
-                const double f = S[i * m + kk] * ip;
-                for (int c = tid & 15; c < ncol; c += 16) {
-                    if (c == ncol - 1) r[i] -= f * r[kk];
-                    else S[i * m + kk + 1 + c] -= f * S[kk * m + kk + 1 + c];
-                }
-            }
-            __syncthreads();
-        }
-        (void)W;
-
-        for (int i = tid; i < m; i += blockDim.x) r[i] = r[i] / S[i * m + i];
-        __syncthreads();
+    if (LARGE) {   // S is the packed system itself (global), r the LDS output
+        if (m <= 48) gj_tiled<3, 4>(S, r, m, tid, &st->error);
+        else if (m <= 64) gj_tiled<4, 5>(S, r, m, tid, &st->error);
+        else if (m <= 96) gj_tiled<6, 7>(S, r, m, tid, &st->error);
+        else gj_tiled<8, 9>(S, r, m, tid, &st->error);
     }
     SSTAMP(a.stamps, 5, 0);
     if (tid < 64) {
@@ -1552,7 +1619,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     STAMPP(a.stamps, 8, 3);
     SolveCtx sc = a.solve;
     sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
-    solve_global(sc, S, r, norms[0], norms[1]);
+    solve_global<false>(sc, S, r, norms[0], norms[1]);
     STAMPP(a.stamps, 8, 7);
 }
 
@@ -1563,6 +1630,10 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;
     double* r = sm + m * m;
+    if (m > 30) {   // the tiled elimination reads the packed system directly
+        solve_global<true>(a.ctx, const_cast<double*>(a.packed), r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+        return;
+    }
     for (int t = tid; t < ntri; t += blockDim.x) {
         int i = 0, rem = t;
         while (rem >= m - i) { rem -= m - i; ++i; }
@@ -1573,7 +1644,7 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     }
     for (int t = tid; t < m; t += blockDim.x) r[t] = a.packed[ntri + t];
     __syncthreads();
-    solve_global(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+    solve_global<false>(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
 }
 
 // ---------------------------------------------------------------- k_backsub
