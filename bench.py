@@ -137,7 +137,7 @@ def main():
 
     # ---- dominant kernel (k_linearize) duration with HIP events on the problem's stream
     ba.timing_begin()
-    ba.step(min(64, max(8, args.steps // 10)))
+    ba.step(min(256, max(8, args.steps // 4)))
     lin_ms, step_ms_ev, nlaunch = ba.timing_end()
     lin_ms = ba.allreduce_max(lin_ms)
     st = ba.stats()

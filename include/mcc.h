@@ -126,7 +126,9 @@ int mcc_comm_barrier(mcc_problem *p);
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
 /* average device time (ms) per launch of the linearisation kernel over the last
- * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches */
+ * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches.
+ * Fused single-GPU problems (m <= 30: one kernel per step) time the whole window of graph-
+ * launched steps with two events; others record an event pair around every launch (eager). */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
 /* diagnostic build only (libmcc_diag.so, -DMCC_DIAG): first call arms per-phase s_memtime
