@@ -785,6 +785,14 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     if (done) return;
     STAMP(0);
     RSTAMP(14);
+#ifdef MCC_DIAG
+    if (tid == 0 && a.stamps) {   // placement: HW_ID (cu/se/simd/wave), XCC_ID; and the edge count
+        const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));
+        a.stamps[kStampStride * (size_t)photo + 25] = ((long long)xcc << 32) | hw;
+        a.stamps[kStampStride * (size_t)photo + 27] = ne;
+    }
+#endif
     extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
     PhotoLds& P = *reinterpret_cast<PhotoLds*>(smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double)));
@@ -1204,6 +1212,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         st_sc1(cv + t, v);
     }
     STAMP(8);
+    RSTAMP(29);
     // ---- level 1: the last photo of a group sums the group in photo order
     const int G = a.group_size, grp = photo / G, g0 = grp * G;
     const int gn = min(G, (int)gridDim.x - g0);
@@ -1218,9 +1227,11 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         st_sc1(a.gsum + (size_t)grp * Lc + t, v);
     }
     STAMP(10);
+    RSTAMP(30);
     // ---- level 2: the last group sums the groups in order -> packed system
     if (!arrive_last_sc1(a.cnt + a.n_groups, a.n_groups)) { RSTAMP(15); return; }
     STAMP(11);
+    RSTAMP(31);
     double* S = smem;            // the edge records are dead: m*m + m doubles for the solve
     double* rr = smem + m * m;
     __shared__ double nrm2[2];

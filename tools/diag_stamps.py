@@ -70,6 +70,33 @@ def main():
         print(f"  timeline (us, 100 MHz): starts spread {(r0.max() - t0) / 100:.2f}; "
               f"exit median {(np.median(r1[ok]) - t0) / 100:.2f}; last exit {(r1[ok].max() - t0) / 100:.2f}")
         print(f"  workgroup residency (us): {med((r1[ok] - r0[ok]) / 100)}")
+        c = s[:, 29]
+        if (c > 0).any():
+            cc = c[c > 0]
+            g = s[s[:, 30] > 0][:, 30]
+            f = s[s[:, 31] > 0][:, 31]
+            print(f"  contributions written (us): first {(cc.min() - t0) / 100:.2f} median {(np.median(cc) - t0) / 100:.2f} "
+                  f"last {(cc.max() - t0) / 100:.2f}; group sums done: last {(g.max() - t0) / 100:.2f}; "
+                  f"final ticket won {(f.max() - t0) / 100:.2f}; end {(r1[ok].max() - t0) / 100:.2f}")
+    # placement / edge count vs linearisation time (slot 25: xcc << 32 | HW_ID, slot 27: edges)
+    hw = s[:, 25].astype(np.int64)
+    if (hw != 0).any():
+        cu = (hw & 0xFFFFFFFF) >> 8 & 0xF
+        sh = (hw & 0xFFFFFFFF) >> 12 & 0x1
+        se = (hw & 0xFFFFFFFF) >> 13 & 0x7
+        xcc = hw >> 32 & 0xF
+        key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+        _, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+        share = cnt[inv]
+        lin = s[:, 7] - s[:, 0]
+        nes = s[:, 27]
+        for n in np.unique(nes):
+            sel = nes == n
+            print(f"  ne={int(n)}: {sel.sum()} photos, linearize {med(lin[sel])}")
+        for k in np.unique(share):
+            sel = share == k
+            print(f"  {int(k)} workgroup(s) on the CU: {sel.sum()} photos, linearize {med(lin[sel])}")
+        print(f"  distinct CUs {len(cnt)}, xcc histogram {np.bincount(xcc.astype(int), minlength=8).tolist()}")
     ok = sch[:, 0] > 0
     if ok.any():
         it = sch[ok]

@@ -1,0 +1,82 @@
+// Micro-benchmark of the reduced-camera-system elimination (gj_dispatch, m <= 30) in isolation.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/gj_bench.hip -o /tmp/gj_bench -lrccl && /tmp/gj_bench [m]
+// One workgroup, wave 1 eliminates a random SPD system REPS times (S reloaded into LDS each time);
+// prints the median s_memtime ticks per elimination and the max relative error vs a host solve.
+#include "../multi_camera_calibration_amd/csrc/mcc_kernels.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+constexpr int REPS = 64;
+
+__global__ void k_gj_bench(const double* Sg, const double* rg, int m, double* xout, long long* ticks, int* err) {
+    __shared__ double S[32 * 32], r[32];
+    const int tid = threadIdx.x;
+    for (int rep = 0; rep < REPS; ++rep) {
+        for (int t = tid; t < m * m; t += blockDim.x) S[t] = Sg[t];
+        for (int t = tid; t < m; t += blockDim.x) r[t] = rg[t];
+        __syncthreads();
+        long long t0 = 0;
+        if (tid == 64) t0 = (long long)__builtin_amdgcn_s_memtime();
+        if (tid >= 64 && tid < 128) mcc::gj_dispatch(S, r, m, tid - 64, err);
+        __syncthreads();
+        if (tid == 64) ticks[rep] = (long long)__builtin_amdgcn_s_memtime() - t0;
+        __syncthreads();
+    }
+    for (int t = tid; t < m; t += blockDim.x) xout[t] = r[t];
+}
+
+int main(int argc, char** argv) {
+    const int m = argc > 1 ? std::atoi(argv[1]) : 18;
+    std::mt19937_64 rng(7);
+    std::normal_distribution<double> nd;
+    std::vector<double> B(m * m), S(m * m, 0.0), r(m);
+    for (auto& v : B) v = nd(rng);
+    for (int i = 0; i < m; ++i)
+        for (int j = 0; j < m; ++j) {
+            double s = (i == j) ? m : 0.0;
+            for (int k = 0; k < m; ++k) s += B[i * m + k] * B[j * m + k];
+            S[i * m + j] = s * 1e6;
+        }
+    for (auto& v : r) v = nd(rng);
+    // host solve (Cholesky)
+    std::vector<double> L(S), x(r);
+    for (int j = 0; j < m; ++j) {
+        double d = L[j * m + j];
+        for (int k = 0; k < j; ++k) d -= L[j * m + k] * L[j * m + k];
+        d = std::sqrt(d);
+        L[j * m + j] = d;
+        for (int i = j + 1; i < m; ++i) {
+            double t = L[i * m + j];
+            for (int k = 0; k < j; ++k) t -= L[i * m + k] * L[j * m + k];
+            L[i * m + j] = t / d;
+        }
+    }
+    for (int i = 0; i < m; ++i) { double t = x[i]; for (int k = 0; k < i; ++k) t -= L[i * m + k] * x[k]; x[i] = t / L[i * m + i]; }
+    for (int i = m - 1; i >= 0; --i) { double t = x[i]; for (int k = i + 1; k < m; ++k) t -= L[k * m + i] * x[k]; x[i] = t / L[i * m + i]; }
+
+    double *dS, *dr, *dx;
+    long long* dt;
+    int* de;
+    hipMalloc(&dS, sizeof(double) * m * m); hipMalloc(&dr, sizeof(double) * m); hipMalloc(&dx, sizeof(double) * m);
+    hipMalloc(&dt, sizeof(long long) * REPS); hipMalloc(&de, sizeof(int));
+    hipMemcpy(dS, S.data(), sizeof(double) * m * m, hipMemcpyHostToDevice);
+    hipMemcpy(dr, r.data(), sizeof(double) * m, hipMemcpyHostToDevice);
+    hipMemset(de, 0, sizeof(int));
+    hipLaunchKernelGGL(k_gj_bench, dim3(1), dim3(256), 0, 0, dS, dr, m, dx, dt, de);
+    if (hipDeviceSynchronize() != hipSuccess) { std::printf("kernel failed\n"); return 1; }
+    std::vector<long long> t(REPS);
+    std::vector<double> xg(m);
+    int e = 0;
+    hipMemcpy(t.data(), dt, sizeof(long long) * REPS, hipMemcpyDeviceToHost);
+    hipMemcpy(xg.data(), dx, sizeof(double) * m, hipMemcpyDeviceToHost);
+    hipMemcpy(&e, de, sizeof(int), hipMemcpyDeviceToHost);
+    std::sort(t.begin() + 1, t.end());
+    double err = 0, xm = 0;
+    for (int i = 0; i < m; ++i) { err = std::max(err, std::fabs(xg[i] - x[i])); xm = std::max(xm, std::fabs(x[i])); }
+    std::printf("m=%d gj median ticks %lld (min %lld, first %lld) rel err %.3e err flags %d\n", m, t[REPS / 2], t[1], t[0], err / xm, e);
+    return 0;
+}
