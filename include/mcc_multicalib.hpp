@@ -1,0 +1,341 @@
+/*
+ * mcc_multicalib.hpp -- C++ host layer over the C ABI (mcc.h), mirroring the reference's operator
+ * interface for the bundle-adjustment path so C++ callers (and the reference's own structure)
+ * use the same names, argument meaning and error behaviour:
+ *
+ *   cv::multicalib::MultiCameraCalibration      include/opencv2/ccalib/multicalib.hpp:73-253
+ *   cv::multicalib::MyMultiCameraCalibration    include/opencv2/ccalib/mymulticalib.hpp:72-180
+ *   cv::multicalib::DoubleSideCalibration       include/opencv2/ccalib/doubleSide.hpp:80-170
+ *
+ * What is mirrored: the problem state loadImages() + initialize() leave behind (_edgeList,
+ * _vertexList, _objectPointsForEachCamera, _imagePointsForEachCamera, _cameraMatrix,
+ * _distortCoeffs, _xi, _criteria, doubleSideTransform, camerasPose), buildParas / paras2vertex
+ * (src/multicalib.cpp:422-459, src/doubleSide.cpp:233-287), optimizeExtrinsics
+ * (src/multicalib.cpp:462-514), the virtual seam computeJacobianExtrinsic (multicalib.hpp:176)
+ * and computeProjectError (multicalib.hpp:188).  cv::Mat becomes std::vector / std::array (no
+ * OpenCV in this build); image loading, pattern detection and initialisation are out of scope
+ * (DESIGN.md section 7): callers fill the state directly.
+ *
+ * Errors: every failing mcc_* call throws std::runtime_error with mcc_last_error() (the
+ * reference's CV_Assert / CV_Error behaviour).  Header-only; link libmcc.so.
+ */
+#ifndef MCC_MULTICALIB_HPP
+#define MCC_MULTICALIB_HPP
+
+#include <array>
+#include <cmath>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mcc.h"
+
+namespace mcc {
+namespace multicalib {
+
+struct TermCriteria {   // cv::TermCriteria: type COUNT (1), EPS (2) or both (3)
+    enum { COUNT = 1, MAX_ITER = COUNT, EPS = 2 };
+    int type = COUNT + EPS;
+    int maxCount = 20;
+    double epsilon = 1e-7;
+    TermCriteria() = default;
+    TermCriteria(int t, int m, double e) : type(t), maxCount(m), epsilon(e) {}
+};
+
+using Pose = std::array<float, 16>;   // 4x4 row-major, CV_32F like the reference's vertex / edge poses
+
+inline Pose eye4() {
+    Pose p{};
+    p[0] = p[5] = p[10] = p[15] = 1.f;
+    return p;
+}
+
+// cvRodrigues2, vector -> matrix, evaluated in double (as OpenCV does) for a float vector
+inline void rodrigues_v2m(const float rv[3], float R[9]) {
+    const double rx = rv[0], ry = rv[1], rz = rv[2];
+    const double th = std::sqrt(rx * rx + ry * ry + rz * rz);
+    if (th < 2.220446049250313e-16) {
+        for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.f : 0.f;
+        return;
+    }
+    const double c = std::cos(th), s = std::sin(th), c1 = 1.0 - c, it = 1.0 / th;
+    const double x = rx * it, y = ry * it, z = rz * it;
+    const double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
+    const double rx_[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+    for (int k = 0; k < 9; ++k) R[k] = (float)(c * ((k % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[k] + s * rx_[k]);
+}
+
+// cvRodrigues2, matrix -> vector (trace / skew formula with the theta ~ 0 and ~ pi branches)
+inline void rodrigues_m2v(const float Rf[9], float rv[3]) {
+    double R[9];
+    for (int k = 0; k < 9; ++k) R[k] = Rf[k];
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = std::acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5; rx = std::sqrt(t > 0 ? t : 0.);
+            t = (R[4] + 1) * 0.5; ry = std::sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5; rz = std::sqrt(t > 0 ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (std::fabs(rx) < std::fabs(ry) && std::fabs(rx) < std::fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            th /= std::sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= th; ry *= th; rz *= th;
+        }
+    } else {
+        const double v = th / (2 * s);
+        rx *= v; ry *= v; rz *= v;
+    }
+    rv[0] = (float)rx; rv[1] = (float)ry; rv[2] = (float)rz;
+}
+
+inline void pose_to_rt(const Pose& P, float r[3], float t[3]) {
+    const float R[9] = {P[0], P[1], P[2], P[4], P[5], P[6], P[8], P[9], P[10]};
+    rodrigues_m2v(R, r);
+    t[0] = P[3]; t[1] = P[7]; t[2] = P[11];
+}
+
+inline Pose rt_to_pose(const float r[3], const float t[3]) {
+    float R[9];
+    rodrigues_v2m(r, R);
+    Pose P = eye4();
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) P[4 * i + j] = R[3 * i + j];
+        P[4 * i + 3] = t[i];
+    }
+    return P;
+}
+
+inline void check(int rc) {
+    if (rc != MCC_OK) throw std::runtime_error(std::string("mcc: ") + mcc_last_error());
+}
+
+class MultiCameraCalibration {
+public:
+    enum { PINHOLE, OMNIDIRECTIONAL };            // multicalib.hpp:76-79
+    enum { FRONT_PATTERN, BACK_PATTERN };         // multicalib.hpp:81-84
+
+    struct edge {                                  // multicalib.hpp:86-101
+        int cameraVertex, photoVertex, photoIndex;
+        int patternSide = FRONT_PATTERN;
+        Pose transform;
+        float reprojecterror = 0.f;
+        edge(int cv, int pv, int pi, const Pose& trans) : cameraVertex(cv), photoVertex(pv), photoIndex(pi), transform(trans) {}
+    };
+    struct vertex {                                // multicalib.hpp:103-122
+        Pose pose = eye4();
+        int timestamp = -1;
+        int timestampCnt = 1;
+        vertex() = default;
+        vertex(const Pose& po, int ts) : pose(po), timestamp(ts) {}
+    };
+
+    MultiCameraCalibration(int cameraType, int nCameras, TermCriteria criteria = TermCriteria(), int device = 0)
+        : _camType(cameraType), _nCamera(nCameras), _criteria(criteria), _device(device),
+          _objectPointsForEachCamera(nCameras), _imagePointsForEachCamera(nCameras), _cameraMatrix(nCameras),
+          _distortCoeffs(nCameras), _xi(nCameras, 0.f) {
+        for (int c = 0; c < nCameras; ++c) _vertexList.emplace_back(eye4(), -1);   // camera vertices
+    }
+    virtual ~MultiCameraCalibration() { release(); }
+    MultiCameraCalibration(const MultiCameraCalibration&) = delete;
+    MultiCameraCalibration& operator=(const MultiCameraCalibration&) = delete;
+
+    // optimizeExtrinsics (src/multicalib.cpp:462-514): the Gauss-Newton loop on the GPU, then
+    // computeProjectError and paras2vertex; returns the reference's meanReProjError
+    double optimizeExtrinsics() {
+        std::vector<float> x = buildParas();
+        check(mcc_optimize(problem(), _criteria.type, _criteria.maxCount, _criteria.epsilon, x.data(), &_iters,
+                           &_change));
+        const double error = computeProjectError(x);
+        paras2vertex(x);
+        return error;
+    }
+
+    // the per-iteration seam (multicalib.hpp:176): deltaX and JTE (P x 1, double) at x;
+    // JTJ_inv is left empty (the reference allocates it and never reads it, mymulticalib.cpp:680)
+    virtual void computeJacobianExtrinsic(const std::vector<float>& extrinsicParams, std::vector<double>& JTJ_inv,
+                                          std::vector<double>& JTE, std::vector<double>& deltaX) {
+        mcc_problem* p = problem();
+        const int P = mcc_nparams(p);
+        if ((int)extrinsicParams.size() != P) throw std::runtime_error("mcc: parameter vector has the wrong size");
+        check(mcc_set_params(p, extrinsicParams.data(), P));
+        JTJ_inv.clear();
+        JTE.assign(P, 0.0);
+        deltaX.assign(P, 0.0);
+        check(mcc_linearize_solve(p, deltaX.data(), JTE.data()));
+    }
+
+    // computeProjectError (multicalib.hpp:188): fills every edge's reprojecterror (per-edge mean
+    // L2 error, float) and returns the reference's mean
+    virtual double computeProjectError(std::vector<float>& parameters) {
+        std::vector<float> err(_edgeList.size());
+        double mean = 0.0;
+        check(mcc_project_error(problem(), parameters.data(), err.data(), &mean));
+        for (size_t e = 0; e < _edgeList.size(); ++e) _edgeList[e].reprojecterror = err[e];
+        return mean;
+    }
+
+    // buildParas (src/multicalib.cpp:422-440): [vertex 1 .. nVertex-1] x (rvec, tvec)
+    virtual std::vector<float> buildParas() {
+        std::vector<float> x;
+        for (size_t v = 1; v < _vertexList.size(); ++v) {
+            float r[3], t[3];
+            pose_to_rt(_vertexList[v].pose, r, t);
+            x.insert(x.end(), r, r + 3);
+            x.insert(x.end(), t, t + 3);
+        }
+        return x;
+    }
+    // paras2vertex (src/multicalib.cpp:442-459)
+    virtual void paras2vertex(const std::vector<float>& x) {
+        for (size_t v = 1; v < _vertexList.size(); ++v)
+            _vertexList[v].pose = rt_to_pose(&x[6 * (v - 1)], &x[6 * (v - 1) + 3]);
+    }
+
+    // drop the device copy of the problem (the next call rebuilds it from the state)
+    void reset() { release(); }
+    int iterations() const { return _iters; }          // Gauss-Newton iterations of the last run
+    double lastChange() const { return _change; }      // change = ||G|| / ||x|| of the last update
+
+    // photo vertex of a timestamp (getPhotoVertex, src/multicalib.cpp:323-346 creates them in
+    // first-appearance order)
+    int addPhotoVertex(int timestamp, const Pose& pose) {
+        _vertexList.emplace_back(pose, timestamp);
+        return (int)_vertexList.size() - 1;
+    }
+
+    // ---- the state loadImages() + initialize() build (multicalib.hpp:193-214)
+    int _camType, _nCamera;
+    TermCriteria _criteria;
+    int _device;
+    std::vector<edge> _edgeList;
+    std::vector<vertex> _vertexList;
+    std::vector<std::vector<std::vector<float>>> _objectPointsForEachCamera;   // [camera][photoIndex]: 3N
+    std::vector<std::vector<std::vector<float>>> _imagePointsForEachCamera;    // [camera][photoIndex]: 2N
+    std::vector<std::array<float, 9>> _cameraMatrix;                           // row-major 3x3
+    std::vector<std::vector<float>> _distortCoeffs;                            // pinhole 4/5/8/12, omni 4
+    std::vector<float> _xi;                                                    // Mei xi (omnidirectional)
+
+protected:
+    virtual int model() const { return _camType == OMNIDIRECTIONAL ? MCC_MODEL_OMNI : MCC_MODEL_PINHOLE; }
+    virtual void extraDesc(mcc_desc&) {}
+
+    mcc_problem* problem() {
+        if (_p) return _p;
+        const int C = _nCamera, E = (int)_edgeList.size();
+        _cam.clear(); _photo.clear(); _side.clear(); _off.clear(); _n.clear();
+        _obj.clear(); _img.clear(); _K.clear(); _D.clear();
+        int corners = 0;
+        for (const edge& e : _edgeList) {
+            if (e.cameraVertex < 0 || e.cameraVertex >= C || e.photoVertex < C || e.photoVertex >= (int)_vertexList.size() ||
+                e.photoIndex < 0 || e.photoIndex >= (int)_objectPointsForEachCamera[e.cameraVertex].size() ||
+                e.photoIndex >= (int)_imagePointsForEachCamera[e.cameraVertex].size())
+                throw std::runtime_error("mcc: edge refers to a missing camera, photo vertex or point set");
+            const std::vector<float>& o = _objectPointsForEachCamera[e.cameraVertex][e.photoIndex];
+            const std::vector<float>& im = _imagePointsForEachCamera[e.cameraVertex][e.photoIndex];
+            const int n = (int)o.size() / 3;
+            if ((int)im.size() != 2 * n) throw std::runtime_error("mcc: object / image point counts differ");
+            _cam.push_back(e.cameraVertex);
+            _photo.push_back(e.photoVertex - C);
+            _side.push_back(e.patternSide);
+            _off.push_back(corners);
+            _n.push_back(n);
+            _obj.insert(_obj.end(), o.begin(), o.end());
+            _img.insert(_img.end(), im.begin(), im.end());
+            corners += n;
+        }
+        const int nd = (int)_distortCoeffs.at(0).size();
+        for (int c = 0; c < C; ++c) {
+            _K.insert(_K.end(), _cameraMatrix[c].begin(), _cameraMatrix[c].end());
+            if ((int)_distortCoeffs[c].size() != nd) throw std::runtime_error("mcc: cameras differ in distortion terms");
+            _D.insert(_D.end(), _distortCoeffs[c].begin(), _distortCoeffs[c].end());
+        }
+        mcc_desc d{};
+        d.model = model();
+        d.n_cams = C;
+        d.n_photos = (int)_vertexList.size() - C;
+        d.n_edges = E;
+        d.edge_cam = _cam.data(); d.edge_photo = _photo.data(); d.edge_side = _side.data();
+        d.edge_off = _off.data(); d.edge_n = _n.data();
+        d.obj = _obj.data(); d.img = _img.data();
+        d.nd = nd; d.K = _K.data(); d.D = _D.data();
+        d.xi = d.model == MCC_MODEL_OMNI ? _xi.data() : nullptr;
+        d.device = _device;
+        extraDesc(d);
+        check(mcc_create(&_p, &d));
+        return _p;
+    }
+    void release() {
+        if (_p) mcc_destroy(_p);
+        _p = nullptr;
+    }
+
+    mcc_problem* _p = nullptr;
+    int _iters = 0;
+    double _change = 0.0;
+    std::vector<int> _cam, _photo, _side, _off, _n;
+    std::vector<float> _obj, _img, _K, _D;
+};
+
+// MyMultiCameraCalibration (mymulticalib.hpp:72-180): pinhole cameras (cv::projectPoints), BACK
+// edges through the fixed doubleSideTransform (mymulticalib.hpp:119-126)
+class MyMultiCameraCalibration : public MultiCameraCalibration {
+public:
+    MyMultiCameraCalibration(int nCameras, TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-7),
+                             int device = 0)
+        : MultiCameraCalibration(PINHOLE, nCameras, criteria, device) {}
+    std::array<double, 16> doubleSideTransform{};   // CV_64F 4x4; all zero = not loaded
+protected:
+    int model() const override { return MCC_MODEL_PINHOLE; }
+    void extraDesc(mcc_desc& d) override {
+        bool any = false;
+        for (double v : doubleSideTransform) any = any || v != 0.0;
+        d.ds_pose = any ? doubleSideTransform.data() : nullptr;
+    }
+};
+
+// DoubleSideCalibration (doubleSide.hpp:80-170): fixed camera poses, the double-side transform is
+// the only global block; parameters [ds, photos] (src/doubleSide.cpp:233-261)
+class DoubleSideCalibration : public MyMultiCameraCalibration {
+public:
+    DoubleSideCalibration(int nCameras, TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-8),
+                          int device = 0)
+        : MyMultiCameraCalibration(nCameras, criteria, device), camerasPose(nCameras, eye4()) {}
+    std::vector<Pose> camerasPose;      // doubleSide.hpp:123
+    Pose doubleSide = eye4();           // the optimised double-side transform (as a pose)
+
+    std::vector<float> buildParas() override {
+        std::vector<float> x(6);
+        pose_to_rt(doubleSide, &x[0], &x[3]);
+        for (size_t v = _nCamera; v < _vertexList.size(); ++v) {
+            float r[3], t[3];
+            pose_to_rt(_vertexList[v].pose, r, t);
+            x.insert(x.end(), r, r + 3);
+            x.insert(x.end(), t, t + 3);
+        }
+        return x;
+    }
+    void paras2vertex(const std::vector<float>& x) override {
+        doubleSide = rt_to_pose(&x[0], &x[3]);
+        for (size_t v = _nCamera; v < _vertexList.size(); ++v) {
+            const size_t o = 6 * (v - _nCamera + 1);
+            _vertexList[v].pose = rt_to_pose(&x[o], &x[o + 3]);
+        }
+    }
+protected:
+    int model() const override { return MCC_MODEL_DOUBLESIDE; }
+    void extraDesc(mcc_desc& d) override {
+        _cp.clear();
+        for (const Pose& P : camerasPose) _cp.insert(_cp.end(), P.begin(), P.end());
+        d.cam_pose = _cp.data();
+    }
+    std::vector<float> _cp;
+};
+
+}  // namespace multicalib
+}  // namespace mcc
+
+#endif

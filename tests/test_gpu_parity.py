@@ -21,6 +21,26 @@ from oracle import oracle_py as O
 
 pytestmark = pytest.mark.gpu
 
+def _widen_distortion(p, nd):
+    """rational (k4..k6) / thin-prism (s1..s4) coefficients on top of the rig's 5 (the k_linearize
+    RATIONAL / PRISM instantiations); observations stay those of the 5-term model."""
+    D = np.zeros((p.n_cams, nd), np.float32)
+    D[:, :min(nd, p.nd)] = p.D[:, :min(nd, p.nd)]
+    extra = [0.01, -0.005, 0.002, 3e-4, -2e-4, 1e-4, 2e-4]
+    for k in range(5, nd):
+        D[:, k] = extra[k - 5]
+    p.D = D
+    return p
+
+
+def _omni_skew():
+    p = rig.make_config("config4", n_views=30)
+    K = p.K.copy()
+    K[:, 0, 1] = 2.5   # skew (src/omnidir.cpp:107, 160)
+    p.K = K
+    return p
+
+
 CASES = {
     "config1": lambda: rig.make_config("config1"),
     "config2_small": lambda: rig.make_config("config2", n_views=60),
@@ -28,6 +48,11 @@ CASES = {
     "config4_small": lambda: rig.make_config("config4", n_views=40),
     "config5_small": lambda: rig.make_config("config5", n_views=30),
     "pinhole_back": lambda: rig.make_config("config5", n_views=30, model=rig.PINHOLE, double_sided=True),
+    "nd4": lambda: _widen_distortion(rig.make_config("config2", n_views=30), 4),
+    "nd8_rational": lambda: _widen_distortion(rig.make_config("config2", n_views=30), 8),
+    "nd12_prism": lambda: _widen_distortion(rig.make_config("config2", n_views=30), 12),
+    "omni_skew": _omni_skew,
+    "cams22_m126": lambda: rig.make_config("config3", n_cams=22, n_views=120),   # largest global block, 19 edges/photo
 }
 
 
