@@ -8,8 +8,15 @@ One "step" = one pass of the hot path over the whole problem: linearisation of e
 (MultiCameraCalibration::optimizeExtrinsics loop body, src/multicalib.cpp:481-506).
 Workload: BASELINE.json configs[1] (4 pinhole cameras, 500 synthetic 11x8-board views) per
 rank; N > 1 ranks (one process per GPU, launched by torch.distributed.run) weak-scale it: the rig
-has 500*N views, photo vertices are sharded and each step does one RCCL all-reduce of the
-reduced camera system.  Rank 0 prints one JSON line.
+has 500*N views, photo vertices are sharded and each step exchanges the reduced camera system
+once: over the peer transport (mcc_peer_*: the final arriving workgroup of each rank writes its
+system into every peer's inbox over xGMI and solves, one kernel per step) when the handshake
+passes on every rank, else with one RCCL all-reduce (MCC_TRANSPORT=rccl forces it).  Rank 0 prints
+one JSON line.
+
+MCC_BENCH_SAME_DEVICE=1 puts every rank on device 0 with the peer transport only (RCCL refuses
+two ranks on one device): a rehearsal of the N > 1 code path on a one-GPU box, not a scaling
+measurement.
 """
 from __future__ import annotations
 
@@ -52,6 +59,36 @@ def rendezvous_id(rank: int, world: int) -> bytes:
         if time.time() - t0 > 300:
             raise RuntimeError("timed out waiting for the RCCL unique id")
         time.sleep(0.05)
+
+
+def setup_transport(ba, rank: int, world: int, same_device: bool) -> str:
+    """RCCL communicator (distinct devices) plus, unless MCC_TRANSPORT=rccl, the peer transport;
+    all ranks agree on the transport over RCCL before it is used."""
+    key = f"/tmp/mcc_peer_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    if not same_device:
+        ba.comm_init(rendezvous_id(rank, world), world, rank)
+    if os.environ.get("MCC_TRANSPORT", "peer") == "rccl":
+        if same_device:
+            raise SystemExit("MCC_BENCH_SAME_DEVICE needs the peer transport")
+        return "rccl"
+    ok = True
+    try:
+        handles = api.file_allgather(key, rank, world, ba.peer_handle())
+        ba.peer_init(handles, world, rank)
+    except api.MccError as e:
+        if same_device:
+            raise
+        print(f"rank {rank}: peer transport unavailable, using RCCL: {e}", file=sys.stderr)
+        ok = False
+    if same_device:
+        return "peer"
+    if ok:
+        ba.peer_enable(False)            # agree over RCCL
+    bad = ba.allreduce_max(0.0 if ok else 1.0)
+    if ok and bad == 0.0:
+        ba.peer_enable(True)
+        return "peer"
+    return "rccl"
 
 
 def load_traffic(config: str, n_views: int):
@@ -111,6 +148,7 @@ def main():
     if world != args.gpus:
         world = args.gpus if "WORLD_SIZE" not in os.environ else world
 
+    same_device = os.environ.get("MCC_BENCH_SAME_DEVICE", "0") == "1"
     api.lib()   # load libmcc.so (and its HIP runtime) before anything else
     views_per_rank = args.views or rig.CONFIGS[args.config]["n_views"]
     full = rig.make_config(args.config, n_views=views_per_rank * world)
@@ -119,9 +157,8 @@ def main():
         prob = rig.subset_photos(full, np.nonzero(owner == rank)[0])
     else:
         prob = full
-    ba = api.BundleAdjuster(prob, device=local_rank)
-    if world > 1:
-        ba.comm_init(rendezvous_id(rank, world), world, rank)
+    ba = api.BundleAdjuster(prob, device=0 if same_device else local_rank)
+    transport = setup_transport(ba, rank, world, same_device) if world > 1 else "none"
     ba.set_params(prob.x0)
 
     # ---- warmup, then exactly K timed steps between barriers
@@ -170,7 +207,10 @@ def main():
                         f"(BASELINE.json configs[1]), one Gauss-Newton step per 'step'",
             "cameras": full.n_cams, "views": full.n_photos, "edges": full.n_edges,
             "corners_per_step": int(corners_total), "params": full.n_params,
-            "parallelism": f"photo-sharded x{world}" + (" + RCCL all-reduce of the camera system" if world > 1 else ""),
+            "parallelism": f"photo-sharded x{world}" + (
+                {"peer": " + in-kernel peer exchange of the camera system (LL words over xGMI)",
+                 "rccl": " + RCCL all-reduce of the camera system"}[transport] if world > 1 else ""),
+            "transport": transport,
             "state_dtype": "f32", "jacobian_dtype": "f64",
         },
         "roofline": {

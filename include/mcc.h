@@ -118,9 +118,28 @@ int mcc_comm_init(mcc_problem *p, const unsigned char *id, int nranks, int rank)
 /* greedy balance of photos over ranks by corner count (descending); rank_of_photo[n_photos] */
 int mcc_partition_photos(int n_photos, int n_edges, const int *edge_photo, const int *edge_n,
                          int nranks, int *rank_of_photo);
-/* collective helpers on the problem's communicator (device-side, blocking) */
+/* collective helpers on the problem's communicator (device-side, blocking); over the peer
+ * transport when it is on or when there is no RCCL communicator */
 int mcc_comm_allreduce_max(mcc_problem *p, double *v);
 int mcc_comm_barrier(mcc_problem *p);
+
+/* ---- peer transport: the step's only exchange without RCCL.  The final arriving workgroup of
+ * every rank writes its packed reduced camera system into every peer's inbox (device memory
+ * mapped by IPC, over xGMI) in LL words (32 data bits + 32-bit epoch per 8-B store) and sums all
+ * ranks' systems in rank order, so every rank solves identical bits in the same kernel; no
+ * all-reduce launch and no k_solve launch per step.  Collective, in this order on every rank:
+ *   mcc_peer_handle(p, h)            -> this rank's inbox handle; exchange them (file, MPI, ...)
+ *   mcc_peer_init(p, all, n, rank)   -> maps the peers, runs a two-round handshake (all ranks
+ *                                       agree: MCC_OK on every rank, or MCC_ECOMM on every rank)
+ * after which the steps use it (mcc_peer_enable(p, 0) falls back to the RCCL communicator).
+ * Works across devices and for several ranks on one device (no RCCL needed).  A rank that does
+ * not deliver within MCC_PEER_TIMEOUT_MS (default 30000) fails the step with MCC_ECOMM. */
+#define MCC_PEER_HANDLE_BYTES 64
+#define MCC_PEER_MAX_RANKS 64
+int mcc_peer_handle(mcc_problem *p, unsigned char *handle /* [64] */);
+int mcc_peer_init(mcc_problem *p, const unsigned char *handles /* [64 * nranks], rank order */, int nranks,
+                  int rank);
+int mcc_peer_enable(mcc_problem *p, int on);
 
 /* ---- diagnostics / measurement */
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */

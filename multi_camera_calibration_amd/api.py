@@ -88,6 +88,9 @@ def lib():
         L.mcc_comm_barrier.argtypes = [ctypes.c_void_p]
         L.mcc_partition_photos.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p]
         L.mcc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+        L.mcc_peer_handle.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.mcc_peer_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.mcc_peer_enable.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -114,6 +117,28 @@ def partition_photos(prob, nranks):
     en = np.ascontiguousarray(prob.edge_n, np.int32)
     _check(lib().mcc_partition_photos(prob.n_photos, prob.n_edges, _ptr(ep, _i32p), _ptr(en, _i32p),
                                       nranks, _ptr(out, _i32p)), "mcc_partition_photos")
+    return out
+
+
+def file_allgather(directory: str, rank: int, world: int, payload: bytes, timeout: float = 300.0) -> list:
+    """All-gather of small byte strings among the processes of one node through files in
+    `directory` (RCCL unique id and peer inbox handles; no torch, no RCCL needed)."""
+    import time
+    os.makedirs(directory, exist_ok=True)
+    tmp = os.path.join(directory, f".r{rank}.tmp")
+    with open(tmp, "wb") as f:
+        f.write(payload)
+    os.replace(tmp, os.path.join(directory, f"r{rank}"))
+    out, t0 = [None] * world, time.time()
+    while any(v is None for v in out):
+        for q in range(world):
+            fn = os.path.join(directory, f"r{q}")
+            if out[q] is None and os.path.exists(fn):
+                with open(fn, "rb") as f:
+                    out[q] = f.read()
+        if time.time() - t0 > timeout:
+            raise MccError(f"timed out waiting for {world} ranks in {directory}")
+        time.sleep(0.02)
     return out
 
 
@@ -253,3 +278,17 @@ class BundleAdjuster:
 
     def barrier(self):
         _check(lib().mcc_comm_barrier(self.h), "mcc_comm_barrier")
+
+    def peer_handle(self) -> bytes:
+        buf = ctypes.create_string_buffer(64)
+        _check(lib().mcc_peer_handle(self.h, buf), "mcc_peer_handle")
+        return buf.raw
+
+    def peer_init(self, handles, nranks: int, rank: int):
+        """Collective: map the peers' inboxes and handshake (raises MccError on every rank if the
+        transport does not work)."""
+        blob = b"".join(handles)
+        _check(lib().mcc_peer_init(self.h, blob, nranks, rank), "mcc_peer_init")
+
+    def peer_enable(self, on: bool):
+        _check(lib().mcc_peer_enable(self.h, int(bool(on))), "mcc_peer_enable")

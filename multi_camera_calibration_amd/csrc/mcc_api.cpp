@@ -139,6 +139,16 @@ struct mcc_problem {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
 
+    // peer transport (mcc_peer_*): LL inbox in uncached device memory, peers' inboxes via IPC
+    static constexpr int kPeerMaxRanks = MCC_PEER_MAX_RANKS;
+    unsigned long long* inbox = nullptr;
+    std::vector<void*> peer_mapped;          // IPC mappings to close
+    unsigned long long** peers_dev = nullptr;
+    double* peer_scratch = nullptr;          // [4] handshake / max
+    int peer_n = 0;                          // ranks of an initialised transport
+    bool peer_on = false;
+    long long peer_timeout = 0;              // s_memrealtime ticks
+
     // timing window
     bool timing = false;
     std::vector<hipEvent_t> ev_lin, ev_step;
@@ -153,6 +163,18 @@ namespace {
 
 mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
     return mcc::SolveCtx{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+}
+
+mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
+    mcc::PeerCtx pc{};
+    if (!on) return pc;
+    pc.inbox = p->inbox;
+    pc.peers = p->peers_dev;
+    pc.nranks = p->peer_n;
+    pc.rank = p->rank;
+    pc.Lc = p->packed_len;
+    pc.timeout = p->peer_timeout;
+    return pc;
 }
 
 int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
@@ -180,23 +202,26 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.dg = p->dg.p;
     la.photo_norm = p->photo_norm.p;
     la.stamps = p->stamps.p;
-    // any communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
-    // split path: the packed system is summed by RCCL and solved by k_solve
-    const bool multi = p->comm != nullptr;
+    // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
+    // split path: the packed system is summed by RCCL and solved by k_solve.  The peer transport
+    // keeps one kernel per step: the final arriver exchanges with the peers and solves.
+    const bool peer = p->peer_on;
+    const bool rccl = p->comm != nullptr && !peer;
     la.fused = p->fused;
     la.group_size = p->group_size; la.n_groups = p->n_groups;
-    la.rank = p->rank; la.fuse_solve = multi ? 0 : 1;
+    la.rank = p->rank; la.fuse_solve = rccl ? 0 : 1;
+    la.peer = peer_ctx(p, peer && p->fused);
     la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p;
     la.solve = solve_ctx(p, do_update);
     la.solve.stamps = nullptr;
     if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
     if (p->fused) {
-        if (multi) {
+        if (rccl) {
             ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                            p->comm, p->stream);
             if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-            SolveArgs so{solve_ctx(p, do_update), p->packed.p};
+            SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false)};
             HIPCHK(mcc_launch_solve(so, p->stream));
         }
         if (tim) {
@@ -217,18 +242,18 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.block_items = p->block_items.p;
     sa.packed = p->packed.p;
     // m > 30: the register-tiled elimination runs in its own kernel (k_solve)
-    const bool split = multi || p->m > 30;
+    const bool split = rccl || peer || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
     sa.solve = solve_ctx(p, do_update);
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
-    if (multi) {
+    if (rccl) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                        p->comm, p->stream);
         if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     }
     if (split) {
-        SolveArgs so{solve_ctx(p, do_update), p->packed.p};
+        SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer)};
         HIPCHK(mcc_launch_solve(so, p->stream));
     }
     if (tim) {
@@ -320,6 +345,7 @@ int read_state(mcc_problem* p) {
 }
 
 int check_state_error(mcc_problem* p) {
+    if (p->h_state->error & 4) return fail(MCC_ECOMM, "peer exchange timed out (a rank did not deliver)");
     if (p->h_state->error & 2) return fail(MCC_ENOTPD, "reduced camera system is not positive definite");
     if (p->h_state->error & 1) return fail(MCC_ENOTPD, "a photo normal-equation block is not positive definite");
     return MCC_OK;
@@ -559,6 +585,10 @@ void mcc_destroy(mcc_problem* p) {
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
     for (auto e : p->ev_win) if (e) (void)hipEventDestroy(e);
     if (p->comm) (void)ncclCommDestroy(p->comm);
+    for (void* m : p->peer_mapped) (void)hipIpcCloseMemHandle(m);
+    if (p->peers_dev) (void)hipFree(p->peers_dev);
+    if (p->peer_scratch) (void)hipFree(p->peer_scratch);
+    if (p->inbox) (void)hipFree(p->inbox);
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
@@ -734,7 +764,7 @@ int mcc_timing_begin(mcc_problem* p) {
         for (auto& e : p->ev_step) HIPCHK(hipEventCreate(&e));
     }
     p->ev_used = 0;
-    if (p->fused && !p->comm) {   // one kernel per step: time the launch window itself (graphs stay on)
+    if (p->fused && (!p->comm || p->peer_on)) {   // one kernel per step: time the launch window itself (graphs stay on)
         if (!p->ev_win[0]) {
             HIPCHK(hipEventCreate(&p->ev_win[0]));
             HIPCHK(hipEventCreate(&p->ev_win[1]));
@@ -817,6 +847,15 @@ int mcc_comm_init(mcc_problem* p, const unsigned char* id, int nranks, int rank)
 
 int mcc_comm_allreduce_max(mcc_problem* p, double* v) {
     if (!p || !v) return fail(MCC_EINVAL, "null argument");
+    if (p->peer_n > 1 && (p->peer_on || !p->comm)) {   // over the peer transport
+        HIPCHK(hipSetDevice(p->device));
+        HIPCHK(hipMemcpyAsync(p->peer_scratch, v, sizeof(double), hipMemcpyHostToDevice, p->stream));
+        HIPCHK(mcc_launch_peer_max(peer_ctx(p, true), p->state.p, p->peer_scratch, p->stream));
+        HIPCHK(hipMemcpyAsync(v, p->peer_scratch, sizeof(double), hipMemcpyDeviceToHost, p->stream));
+        int rc = read_state(p);
+        if (rc) return rc;
+        return check_state_error(p);
+    }
     if (!p->comm || p->nranks == 1) return MCC_OK;
     HIPCHK(hipSetDevice(p->device));
     double* dv;
@@ -835,6 +874,79 @@ int mcc_comm_barrier(mcc_problem* p) {
     int rc = mcc_comm_allreduce_max(p, &v);
     if (rc) return rc;
     HIPCHK(hipDeviceSynchronize());
+    return MCC_OK;
+}
+
+int mcc_peer_handle(mcc_problem* p, unsigned char* handle) {
+    if (!p || !handle) return fail(MCC_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    if (!p->inbox) {
+        const size_t words = (size_t)2 * mcc_problem::kPeerMaxRanks * 2 * (size_t)p->packed_len;
+        HIPCHK(hipExtMallocWithFlags((void**)&p->inbox, words * sizeof(unsigned long long), hipDeviceMallocUncached));
+        HIPCHK(hipMemset(p->inbox, 0, words * sizeof(unsigned long long)));   // epoch 0 is never sent
+        HIPCHK(hipMalloc((void**)&p->peer_scratch, 4 * sizeof(double)));
+        HIPCHK(hipDeviceSynchronize());
+    }
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, p->inbox));
+    static_assert(sizeof(h) == MCC_PEER_HANDLE_BYTES, "IPC handle size");
+    std::memcpy(handle, &h, MCC_PEER_HANDLE_BYTES);
+    return MCC_OK;
+}
+
+int mcc_peer_init(mcc_problem* p, const unsigned char* handles, int nranks, int rank) {
+    if (!p || !handles || nranks < 1 || nranks > mcc_problem::kPeerMaxRanks || rank < 0 || rank >= nranks)
+        return fail(MCC_EINVAL, "bad peer arguments");
+    if (!p->inbox) return fail(MCC_EINVAL, "mcc_peer_handle must be called first");
+    if (p->V == 0) return fail(MCC_EINVAL, "a rank of the peer transport needs photos");
+    if (p->peer_n) return fail(MCC_EINVAL, "peer transport already initialised");
+    if (p->comm && (p->rank != rank || p->nranks != nranks)) return fail(MCC_EINVAL, "rank differs from the RCCL one");
+    HIPCHK(hipSetDevice(p->device));
+    std::vector<unsigned long long*> ptrs(nranks, nullptr);
+    for (int q = 0; q < nranks; ++q) {
+        if (q == rank) { ptrs[q] = p->inbox; continue; }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)q * MCC_PEER_HANDLE_BYTES, MCC_PEER_HANDLE_BYTES);
+        void* m = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(MCC_ECOMM, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        p->peer_mapped.push_back(m);
+        ptrs[q] = (unsigned long long*)m;
+    }
+    if (!p->peers_dev) HIPCHK(hipMalloc((void**)&p->peers_dev, mcc_problem::kPeerMaxRanks * sizeof(void*)));
+    HIPCHK(hipMemcpy(p->peers_dev, ptrs.data(), nranks * sizeof(void*), hipMemcpyHostToDevice));
+    double ms = 30000.0;
+    if (const char* t = std::getenv("MCC_PEER_TIMEOUT_MS")) ms = std::max(1.0, std::atof(t));
+    p->peer_timeout = (long long)(ms * 1e5);   // s_memrealtime: 100 MHz
+    p->peer_n = nranks;
+    p->rank = rank;
+    p->nranks = nranks;
+    HIPCHK(mcc_launch_peer_handshake(peer_ctx(p, true), p->state.p, p->peer_scratch, p->stream));
+    double out[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(out, p->peer_scratch, sizeof(out), hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    if (out[0] != 1.0) {
+        p->peer_n = 0;
+        return fail(MCC_ECOMM, "peer handshake failed: mismatches " + std::to_string((long long)out[1]) +
+                                   ", round-1 timeout " + std::to_string((int)out[2]) + ", round-2 timeout " +
+                                   std::to_string((int)out[3]));
+    }
+    p->peer_on = true;
+    for (auto& g : p->gexec)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    return MCC_OK;
+}
+
+int mcc_peer_enable(mcc_problem* p, int on) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    if (on && !p->peer_n) return fail(MCC_EINVAL, "peer transport not initialised");
+    if (!on && !p->comm && p->peer_n > 1) return fail(MCC_EINVAL, "no RCCL communicator to fall back to");
+    if (p->peer_on != (on != 0)) {
+        HIPCHK(hipStreamSynchronize(p->stream));
+        for (auto& g : p->gexec)
+            if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    }
+    p->peer_on = on != 0;
     return MCC_OK;
 }
 

@@ -19,8 +19,23 @@ struct State {
     double change;    // ||G|| / ||x|| of the last update
     double alpha;     // 0.95^(k+1) of the running step
     double cam_normG2, cam_normX2;   // global-block partials of the last update
-    int error;        // bit 0: photo block not PD, bit 1: camera system not PD
+    int error;        // bit 0: photo block not PD, bit 1: camera system not PD, bit 2: peer timeout
     int pending;      // a solved photo update waits to be applied by the next k_linearize
+    unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
+};
+
+// Peer transport (multi-GPU without RCCL in the step): every rank's final arriver writes its packed
+// reduced system straight into every peer's inbox over xGMI, then sums all ranks' systems in rank
+// order.  LL format (the RCCL low-latency protocol's idea): each 8-B word carries 32 data bits and
+// the 32-bit epoch of the exchange, so a reader needs no cross-device ordering or fence, only the
+// 8-B single-copy atomicity of an aligned store.  Inbox: [2 slots (epoch parity)][nranks][2 Lc]
+// words in uncached device memory; peers[q] is rank q's inbox mapped into this process (IPC).
+struct PeerCtx {
+    unsigned long long* inbox;
+    unsigned long long* const* peers;   // [nranks] device array (peers[rank] == inbox)
+    int nranks;                         // 0: transport off
+    int rank, Lc;
+    long long timeout;                  // s_memrealtime ticks (100 MHz)
 };
 
 struct SolveCtx {
@@ -69,6 +84,7 @@ struct LinArgs {
     int* cnt;                // [n_groups + 1] tickets, zero between launches
     double* packed;          // [Lc]
     SolveCtx solve;
+    PeerCtx peer;            // nranks > 0: the final arriver exchanges with the peers and solves
 };
 
 struct SchurArgs {
@@ -89,7 +105,8 @@ struct SchurArgs {
 
 struct SolveArgs {
     SolveCtx ctx;
-    const double* packed;
+    double* packed;
+    PeerCtx peer;            // nranks > 0: exchange the packed system with the peers first
 };
 
 struct BacksubArgs {
@@ -125,4 +142,6 @@ hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, 
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
+hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);
+hipError_t mcc_launch_peer_max(const mcc::PeerCtx& pc, mcc::State* st, double* v, hipStream_t s);
 hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s);

@@ -767,6 +767,80 @@ __device__ __forceinline__ double sum_sc1(const double* p, int n, size_t stride)
     return v;
 }
 
+// ---------------------------------------------------------------- peer transport (PeerCtx)
+// System-scope relaxed 8-B stores / loads (global_store / global_load sc0 sc1): write-through to
+// the owner's memory over xGMI, reads from memory (the inbox is uncached besides).  No fence: an
+// LL word is valid on its own once its epoch half matches.
+__device__ __forceinline__ void st_sys(unsigned long long* p, unsigned long long w) {
+    __hip_atomic_store((gu64*)p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ size_t peer_word(const PeerCtx& pc, unsigned ep, int src, int t) {
+    return ((size_t)(ep & 1u) * pc.nranks + src) * 2 * (size_t)pc.Lc + 2 * (size_t)t;
+}
+// value t of this rank -> every peer's inbox (two LL words: low and high 32 bits)
+__device__ __forceinline__ void peer_send(const PeerCtx& pc, unsigned ep, int t, double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v), e = (unsigned long long)ep << 32;
+    const size_t w = peer_word(pc, ep, pc.rank, t);
+    for (int q = 0; q < pc.nranks; ++q) {
+        if (q == pc.rank) continue;
+        unsigned long long* d = pc.peers[q] + w;
+        st_sys(d, e | (b & 0xffffffffull));
+        st_sys(d + 1, e | (b >> 32));
+    }
+}
+// value t of rank q from this rank's inbox; spins until both words carry epoch ep, or gives up
+// (timeout set, returns 0) once t0 + pc.timeout has passed
+__device__ __forceinline__ double peer_recv(const PeerCtx& pc, unsigned ep, int q, int t, long long t0, bool& timeout) {
+    const unsigned long long* s = pc.inbox + peer_word(pc, ep, q, t);
+    for (;;) {
+        const unsigned long long a = ld_sys(s), b = ld_sys(s + 1);
+        if ((unsigned)(a >> 32) == ep && (unsigned)(b >> 32) == ep)
+            return __longlong_as_double((long long)(((b & 0xffffffffull) << 32) | (a & 0xffffffffull)));
+        if (timeout || (long long)__builtin_amdgcn_s_memrealtime() - t0 > pc.timeout) {
+            timeout = true;
+            return 0.0;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+// sum over ranks in rank order (identical bits on every rank); own = this rank's value
+__device__ __forceinline__ double peer_sum(const PeerCtx& pc, unsigned ep, int t, double own, long long t0, bool& timeout) {
+    double s = 0.0;
+    for (int q = 0; q < pc.nranks; ++q) s += q == pc.rank ? own : peer_recv(pc, ep, q, t, t0, timeout);
+    return s;
+}
+// The exchange of the packed system held in vals[0, Lc) (global, this workgroup's own copy):
+// every thread sends its entries, then replaces them with the rank-ordered sums.  Returns false
+// (state error bit 2, done) when a peer did not deliver within the timeout.  Whole workgroup.
+__device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, double* vals) {
+    __shared__ unsigned ep_s;
+    __shared__ int to_s;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        ep_s = st->epoch + 1u;
+        to_s = 0;
+    }
+    __syncthreads();
+    const unsigned ep = ep_s;
+    for (int t = tid; t < pc.Lc; t += blockDim.x) peer_send(pc, ep, t, vals[t]);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool timeout = false;
+    for (int t = tid; t < pc.Lc; t += blockDim.x) vals[t] = peer_sum(pc, ep, t, vals[t], t0, timeout);
+    if (timeout) to_s = 1;
+    __syncthreads();
+    if (tid == 0) {
+        st->epoch = ep;
+        if (to_s) {
+            st->error |= 4;
+            st->done = 1;
+        }
+    }
+    return !to_s;
+}
+
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2);
 
@@ -1238,9 +1312,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     const int iter0 = P.iter0;   // read before S overwrites the photo record
     const double cnG = P.cn[0], cnX = P.cn[1];
     __syncthreads();
-    for (int t = tid; t < Lc; t += blockDim.x) {
-        double v = 0.0;
-        v = sum_sc1(a.gsum + t, a.n_groups, Lc);
+    auto place = [&](int t, double v) {
         if (t < ntri) {
             int i, j;
             packed_ij(t, m, i, j);
@@ -1248,16 +1320,28 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             S[j * m + i] = v;
         } else if (t < ntri + m) {
             rr[t - ntri] = v;
-        } else if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
+        } else if (t >= ntri + 2 * m) {
+            nrm2[t - ntri - 2 * m] = v;
+        }
+    };
+    const bool peer = a.peer.nranks > 0;
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        v = sum_sc1(a.gsum + t, a.n_groups, Lc);
+        if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
             const int w = t - ntri - 2 * m;
             if (iter0 > 0) {
                 if (a.rank == 0) v += w ? cnX : cnG;
             } else {
                 v = 0.0;
             }
-            nrm2[w] = v;
         }
+        if (!peer) place(t, v);
         a.packed[t] = v;
+    }
+    if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
+        if (!peer_exchange(a.peer, st, a.packed)) { RSTAMP(15); return; }
+        for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);
     }
     if (!a.fuse_solve) { RSTAMP(15); return; }
     __syncthreads();
@@ -1641,8 +1725,9 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;
     double* r = sm + m * m;
+    if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed)) return;
     if (m > 30) {   // the tiled elimination reads the packed system directly
-        solve_global<true>(a.ctx, const_cast<double*>(a.packed), r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+        solve_global<true>(a.ctx, a.packed, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
         return;
     }
     for (int t = tid; t < ntri; t += blockDim.x) {
@@ -1656,6 +1741,72 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     for (int t = tid; t < m; t += blockDim.x) r[t] = a.packed[ntri + t];
     __syncthreads();
     solve_global<false>(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+}
+
+// ---------------------------------------------------------------- peer transport: handshake, max
+// k_peer_handshake: round 1 sends a (rank, index) pattern over the whole inbox width and checks
+// every peer's; round 2 sends each rank's verdict, so all ranks reach the same one (out[0] = 1 only
+// if every rank saw every peer's pattern intact).  out = {all_ok, mismatches, round-1 timeout,
+// round-2 timeout}.  One workgroup.
+__device__ __forceinline__ double peer_pattern(int rank, int t) {
+    return (double)(rank + 1) * 1.0e6 + (double)t * 0.123456789 + 1.0 / 3.0;
+}
+__global__ __launch_bounds__(256) void k_peer_handshake(PeerCtx pc, State* st, double* out) {
+    __shared__ unsigned ep_s;
+    __shared__ int bad_s, to_s;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        ep_s = st->epoch + 1u;
+        bad_s = 0;
+        to_s = 0;
+    }
+    __syncthreads();
+    const unsigned ep = ep_s;
+    for (int t = tid; t < pc.Lc; t += blockDim.x) peer_send(pc, ep, t, peer_pattern(pc.rank, t));
+    long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool to = false;
+    int bad = 0;
+    for (int q = 0; q < pc.nranks; ++q) {
+        if (q == pc.rank) continue;
+        for (int t = tid; t < pc.Lc; t += blockDim.x) {
+            const double v = peer_recv(pc, ep, q, t, t0, to);
+            if (!to && v != peer_pattern(q, t)) ++bad;
+        }
+    }
+    if (bad) atomicAdd(&bad_s, bad);
+    if (to) to_s = 1;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned ep2 = ep + 1u;
+        const double ok = (bad_s == 0 && to_s == 0) ? 1.0 : 0.0;
+        peer_send(pc, ep2, 0, ok);
+        bool to2 = false;
+        double all = ok;
+        t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (int q = 0; q < pc.nranks; ++q)
+            if (q != pc.rank) all = fmin(all, peer_recv(pc, ep2, q, 0, t0, to2));
+        out[0] = to2 ? 0.0 : all;
+        out[1] = (double)bad_s;
+        out[2] = (double)to_s;
+        out[3] = to2 ? 1.0 : 0.0;
+        st->epoch = ep2;
+    }
+}
+
+// k_peer_max: v[0] <- max over ranks (the bench's max-over-ranks timing and the barrier when no
+// RCCL communicator exists, e.g. several ranks on one device).  One thread.
+__global__ void k_peer_max(PeerCtx pc, State* st, double* v) {
+    if (threadIdx.x != 0) return;
+    const unsigned ep = st->epoch + 1u;
+    peer_send(pc, ep, 0, v[0]);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool to = false;
+    double mx = v[0];
+    for (int q = 0; q < pc.nranks; ++q)
+        if (q != pc.rank) mx = fmax(mx, peer_recv(pc, ep, q, 0, t0, to));
+    v[0] = mx;
+    st->epoch = ep;
+    if (to) st->error |= 4;
 }
 
 // ---------------------------------------------------------------- k_backsub
@@ -1864,6 +2015,14 @@ hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
 }
 hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), mcc_solve_shmem(a.ctx.m), s, a);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_peer_handshake(const PeerCtx& pc, State* st, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_peer_handshake, dim3(1), dim3(256), 0, s, pc, st, out);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_peer_max(const PeerCtx& pc, State* st, double* v, hipStream_t s) {
+    hipLaunchKernelGGL(k_peer_max, dim3(1), dim3(64), 0, s, pc, st, v);
     return hipGetLastError();
 }
 hipError_t mcc_launch_backsub(const BacksubArgs& a, hipStream_t s) {

@@ -1,0 +1,61 @@
+"""Worker for tests/test_peer_transport.py: one rank of the photo-sharded Gauss-Newton step over the
+peer transport (mcc_peer_*), several ranks on ONE device (RCCL refuses that; the peer transport
+does not need it).  No torch: the inbox handles travel through files (api.file_allgather).
+
+    python tests/peer_worker.py <case> <rank> <world> <rendezvous dir> <out.npz> [steps]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from multi_camera_calibration_amd import api, rig  # noqa: E402
+
+CASES = {
+    # fused single-kernel step (m = 18): the final arriver exchanges and solves
+    "config2_small": lambda: rig.make_config("config2", n_views=40),
+    # DoubleSide (m = 6), fused
+    "config5_small": lambda: rig.make_config("config5", n_views=24),
+    # m = 90: k_linearize + k_schur, the exchange runs in k_solve
+    "config3_small": lambda: rig.make_config("config3", n_views=48),
+}
+
+
+def shard(case, world, rank):
+    p = CASES[case]()
+    owner = api.partition_photos(p, world)
+    mine = np.nonzero(owner == rank)[0]
+    return p, mine, rig.subset_photos(p, mine)
+
+
+def main():
+    case, rank, world, rdv, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
+    steps = int(sys.argv[6]) if len(sys.argv) > 6 else 100
+    p, mine, q = shard(case, world, rank)
+    ba = api.BundleAdjuster(q, device=0)
+    handles = api.file_allgather(os.path.join(rdv, "handles"), rank, world, ba.peer_handle())
+    ba.peer_init(handles, world, rank)
+    mx = ba.allreduce_max(rank + 0.5)
+    d, j = ba.compute_jacobian_extrinsic(q.x0)
+    x, _, it, ch = ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=1e-7)
+    # throughput of unconditional steps (the bench's loop) over the transport
+    ba.set_params(q.x0)
+    ba.step(10)
+    ba.synchronize()
+    ba.barrier()
+    t0 = time.perf_counter()
+    ba.step(steps)
+    ba.synchronize()
+    ba.barrier()
+    dt = ba.allreduce_max(time.perf_counter() - t0)
+    ba.close()
+    np.savez(out, mine=mine, x=x, it=it, ch=ch, d=d, j=j, mx=mx, ms=dt / steps * 1e3)
+
+
+if __name__ == "__main__":
+    main()
