@@ -123,7 +123,7 @@ struct mcc_problem {
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
-    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum;
+    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
@@ -211,7 +211,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.group_size = p->group_size; la.n_groups = p->n_groups;
     la.rank = p->rank; la.fuse_solve = rccl ? 0 : 1;
     la.peer = peer_ctx(p, peer && p->fused);
-    la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p;
+    la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p; la.W = p->W.p;
     la.solve = solve_ctx(p, do_update);
     la.solve.stamps = nullptr;
     if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
@@ -555,6 +555,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (p->fused) {
         HIPC(p->contrib.alloc((size_t)p->packed_len * std::max(V, 1)));
         HIPC(p->gsum.alloc((size_t)p->packed_len * p->n_groups));
+        HIPC(p->W.alloc((size_t)6 * p->m * std::max(V, 1)));
         HIPC(p->cnt.alloc(p->n_groups + 1));
         HIPC(hipMemset(p->cnt.p, 0, sizeof(int) * (p->n_groups + 1)));
     }
@@ -592,7 +593,7 @@ void mcc_destroy(mcc_problem* p) {
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
-    p->contrib.release(); p->gsum.release(); p->cnt.release();
+    p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Hgp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();

@@ -83,6 +83,7 @@ struct LinArgs {
     double* gsum;            // [n_groups * Lc]
     int* cnt;                // [n_groups + 1] tickets, zero between launches
     double* packed;          // [Lc]
+    double* W;               // [V * 6m] per-photo pending-update matrix (next step's phase 0)
     SolveCtx solve;
     PeerCtx peer;            // nranks > 0: the final arriver exchanges with the peers and solves
 };

@@ -887,7 +887,25 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
         else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
         else if (lane == 10) P.iter0 = st->iter;
-        if (pending) {
+        if (pending && a.fused) {
+            if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
+            // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
+            // W (written by the previous step) is indexed by the photo alone, so every operand
+            // of the pending update arrives in this first round trip.
+            const int k = lane % 6, c = lane / 6, m = a.global_dim;
+            if (lane < 60) {
+                const double* Wk = a.W + (size_t)photo * 6 * m + (size_t)k * m;
+                double w[3], d[3];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const int col = c + 10 * u;
+                    w[u] = col < m ? Wk[col] : 0.0;
+                    d[u] = col < m ? a.dg[col] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 3; ++u) part += w[u] * d[u];
+            }
+        } else if (pending) {
             if (lane >= 42 && lane < 48) lov = a.zp[6 * (size_t)photo + lane - 42];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, edges l / 6, l / 6 + 10, ...: sum_i Y_e[i][k] dg_{g(e)}[i].
             // The first edge's Y column and block are loaded before dg is staged, so the two
@@ -985,7 +1003,24 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     }
     STAMP(16);
     if (wave == 0) {
-        if (pending) {
+        if (pending && a.fused) {
+            // fused back-substitution of the previous step: dp_k = z'_k - sum_c part(k, c),
+            // the ten partials of component k summed in c order through LDS by lane k
+            if (lane < 60) P.dgl[lane] = part;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < 6) {
+                double tq = lov;
+#pragma unroll
+                for (int c = 0; c < 10; ++c) tq -= P.dgl[6 * c + lane];
+                const float G = (float)(alpha_prev * tq);   // G = alpha*delta -> CV_32F (:491-496)
+                const float xn = xov + G;                   // x = x + G (:501)
+                xg[lane] = xn;
+                P.xp[lane] = xn;
+                P.dgl[64 + lane] = (double)G;
+            }
+        } else if (pending) {
             // fused back-substitution of the previous step: dp = z' - sum_e Y_e^T dg_e,
             // operands gathered from wave 0's registers with compile-time v_readlane
             double t[6];
@@ -1017,6 +1052,18 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         STAMP(18);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
+            if (pending && a.fused) {   // norms of the applied update (independent of the Rodrigues chain)
+                double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    g2 += P.dgl[64 + q] * P.dgl[64 + q];
+                    x2 += P.xp[q] * P.xp[q];
+                }
+                a.photo_norm[2 * (size_t)photo] = g2;
+                a.photo_norm[2 * (size_t)photo + 1] = x2;
+                P.nrm[0] = g2;
+                P.nrm[1] = x2;
+            }
             const double om1[3] = {P.xp[0], P.xp[1], P.xp[2]};
             Rot r1;
             rodrigues_v2m(om1, r1);
@@ -1290,7 +1337,16 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     // ---- level 1: the last photo of a group sums the group in photo order
     const int G = a.group_size, grp = photo / G, g0 = grp * G;
     const int gn = min(G, (int)gridDim.x - g0);
-    if (!arrive_last_sc1(a.cnt + grp, gn, a.stamps ? a.stamps + kStampStride * (size_t)photo + 28 : nullptr)) {
+    const bool grp_last = arrive_last_sc1(a.cnt + grp, gn, a.stamps ? a.stamps + kStampStride * (size_t)photo + 28 : nullptr);
+    // the next step's pending-update matrix of this photo (after the ticket: off its drain),
+    // W[k][6g + i] = sum over the photo's edges e of camera block g of Y'_e[i][k]
+    for (int t = tid; t < 6 * m; t += blockDim.x) {
+        const int k = t / m, col = t % m, g = col / 6, i = col % 6;
+        double w = 0.0;
+        for (int q = 0; q < P.bn[g]; ++q) w += el[P.bl[g][q]].Xg[i * 6 + k];
+        a.W[(size_t)photo * 6 * m + t] = w;
+    }
+    if (!grp_last) {
         RSTAMP(15);
         return;
     }
