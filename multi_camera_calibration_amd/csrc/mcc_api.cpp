@@ -267,7 +267,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
 // pending update (do_update = 1)
 int enqueue_backsub(mcc_problem* p, int do_update) {
     mcc::BacksubArgs ba{p->state.p, p->photo_ptr.p, p->edge_gblock.p, p->Y.p, p->zp.p, p->dg.p,
-                        p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
+                        p->fused ? p->W.p : nullptr, p->x.p, p->delta.p, p->photo_norm.p, p->V, p->m, do_update};
     HIPCHK(mcc_launch_backsub(ba, p->stream));
     return MCC_OK;
 }

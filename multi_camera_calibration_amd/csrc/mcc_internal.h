@@ -115,6 +115,7 @@ struct BacksubArgs {
     const int* photo_ptr;
     const int* gblock;
     const double* Y; const double* zp; const double* dg;
+    const double* W;         // fused path: per-photo pending-update matrix (else nullptr: Y)
     float* x;
     double* delta;
     double* photo_norm;

@@ -692,6 +692,19 @@ __device__ __forceinline__ void photo_delta(const int* photo_ptr, const int* gbl
     }
 }
 
+// fused path: dp = z - W dg with the photo's 6 x m pending-update matrix (k_linearize phase E)
+__device__ __forceinline__ void photo_delta_w(const double* W, int m, const double* zp, const double* dg, int p,
+                                             double t[6]) {
+    const double* z = zp + 6 * (size_t)p;
+    const double* Wp = W + (size_t)p * 6 * m;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        double s = 0.0;
+        for (int c = 0; c < m; ++c) s += Wp[k * m + c] * dg[c];
+        t[k] = z[k] - s;
+    }
+}
+
 // ---------------------------------------------------------------- cross-workgroup hand-off
 // Publish this workgroup's global stores and take a ticket; returns true (uniformly) in the
 // last of `expected` arrivals, which then sees every other arrival's stores.  Agent-scope
@@ -1258,10 +1271,10 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) y += L.Hgp[i * 6 + k] * Hi[k * 6 + j];
         }
-        a.Y[36 * e + ij] = y;
-        if (a.fused) {
+        if (a.fused) {   // (W below replaces the edge-indexed Y' of the split path)
             L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the contribution below
         } else {
+            a.Y[36 * e + ij] = y;
             a.Hgg[36 * e + ij] = L.has_global ? L.Hgg[ij] : 0.0;
             a.Hgp[36 * e + ij] = L.has_global ? L.Hgp[ij] : 0.0;
             if (j == 0) a.gg[6 * e + i] = L.has_global ? L.gg[i] : 0.0;
@@ -1872,7 +1885,8 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n_photos) return;
     double t[6];
-    photo_delta(a.photo_ptr, a.gblock, a.Y, a.zp, a.dg, p, t);
+    if (a.W) photo_delta_w(a.W, a.m, a.zp, a.dg, p, t);
+    else photo_delta(a.photo_ptr, a.gblock, a.Y, a.zp, a.dg, p, t);
     const int col = a.m + 6 * p;
     const double alpha = a.state->alpha;
     double g2 = 0.0, x2 = 0.0;
