@@ -7,23 +7,32 @@
  *   cv::multicalib::MyMultiCameraCalibration    include/opencv2/ccalib/mymulticalib.hpp:72-180
  *   cv::multicalib::DoubleSideCalibration       include/opencv2/ccalib/doubleSide.hpp:80-170
  *
- * What is mirrored: the problem state loadImages() + initialize() leave behind (_edgeList,
- * _vertexList, _objectPointsForEachCamera, _imagePointsForEachCamera, _cameraMatrix,
- * _distortCoeffs, _xi, _criteria, doubleSideTransform, camerasPose), buildParas / paras2vertex
- * (src/multicalib.cpp:422-459, src/doubleSide.cpp:233-287), optimizeExtrinsics
- * (src/multicalib.cpp:462-514), the virtual seam computeJacobianExtrinsic (multicalib.hpp:176)
- * and computeProjectError (multicalib.hpp:188).  cv::Mat becomes std::vector / std::array (no
- * OpenCV in this build); image loading, pattern detection and initialisation are out of scope
- * (DESIGN.md section 7): callers fill the state directly.
+ * What is mirrored:
+ *   - the problem state loadImages() + initialize() build (_edgeList, _vertexList,
+ *     _objectPointsForEachCamera, _imagePointsForEachCamera, _cameraMatrix, _distortCoeffs, _xi,
+ *     _criteria, doubleSideTransform, camerasPose);
+ *   - buildParas / paras2vertex (src/multicalib.cpp:422-459, src/doubleSide.cpp:233-287),
+ *     optimizeExtrinsics (src/multicalib.cpp:462-514), the virtual seam computeJacobianExtrinsic
+ *     (multicalib.hpp:176) and computeProjectError (multicalib.hpp:188): inline here, on libmcc.so;
+ *   - the sample's problem construction and driver, in libmcc_host.so
+ *     (multi_camera_calibration_amd/host/multicalib.cpp): MyMultiCameraCalibration's reference
+ *     constructor (camera configs, double-side transform), loadImages(outliers) (corner files,
+ *     solvePnP initialisation, multi-camera timestamp filter, edges), initialize() (graph BFS
+ *     pose chaining), removeOutlier(), reset(), run(), writeParameters() (+ the camera-config
+ *     rewrite).  cv::FileStorage and cv::solvePnP are restated in mcc_storage.hpp / mcc_pnp.hpp.
+ * cv::Mat becomes std::vector / std::array (no OpenCV in this build).  Out of scope: image
+ * decoding and pattern detection (the reference reads pre-detected corners from files too).
  *
  * Errors: every failing mcc_* call throws std::runtime_error with mcc_last_error() (the
- * reference's CV_Assert / CV_Error behaviour).  Header-only; link libmcc.so.
+ * reference's CV_Assert / CV_Error behaviour).  Link libmcc.so (and libmcc_host.so for the
+ * loaders / writers).
  */
 #ifndef MCC_MULTICALIB_HPP
 #define MCC_MULTICALIB_HPP
 
 #include <array>
 #include <cmath>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -40,6 +49,12 @@ struct TermCriteria {   // cv::TermCriteria: type COUNT (1), EPS (2) or both (3)
     double epsilon = 1e-7;
     TermCriteria() = default;
     TermCriteria(int t, int m, double e) : type(t), maxCount(m), epsilon(e) {}
+};
+
+struct Size {   // cv::Size
+    int width = 0, height = 0;
+    Size() = default;
+    Size(int w, int h) : width(w), height(h) {}
 };
 
 using Pose = std::array<float, 16>;   // 4x4 row-major, CV_32F like the reference's vertex / edge poses
@@ -136,7 +151,8 @@ public:
     MultiCameraCalibration(int cameraType, int nCameras, TermCriteria criteria = TermCriteria(), int device = 0)
         : _camType(cameraType), _nCamera(nCameras), _criteria(criteria), _device(device),
           _objectPointsForEachCamera(nCameras), _imagePointsForEachCamera(nCameras), _cameraMatrix(nCameras),
-          _distortCoeffs(nCameras), _xi(nCameras, 0.f) {
+          _distortCoeffs(nCameras), _xi(nCameras, 0.f), filesEachCameraFull(nCameras), timestampFull(nCameras),
+          timestampAvailable(nCameras), _omEachCamera(nCameras), _tEachCamera(nCameras) {
         for (int c = 0; c < nCameras; ++c) _vertexList.emplace_back(eye4(), -1);   // camera vertices
     }
     virtual ~MultiCameraCalibration() { release(); }
@@ -144,15 +160,32 @@ public:
     MultiCameraCalibration& operator=(const MultiCameraCalibration&) = delete;
 
     // optimizeExtrinsics (src/multicalib.cpp:462-514): the Gauss-Newton loop on the GPU, then
-    // computeProjectError and paras2vertex; returns the reference's meanReProjError
+    // computeProjectError and paras2vertex; returns the reference's meanReProjError (also kept
+    // in _error for writeParameters)
     double optimizeExtrinsics() {
         std::vector<float> x = buildParas();
         check(mcc_optimize(problem(), _criteria.type, _criteria.maxCount, _criteria.epsilon, x.data(), &_iters,
                            &_change));
         const double error = computeProjectError(x);
         paras2vertex(x);
+        _error = error;
         return error;
     }
+
+    // ---- the sample's driver (libmcc_host.so)
+    // loadImages + initialize + optimizeExtrinsics (src/multicalib.cpp:127-133)
+    virtual double run();
+    // the base class's random-pattern loader is out of scope (feature matching on images):
+    // throws; MyMultiCameraCalibration::loadImages reads pre-detected corners
+    virtual void loadImages();
+    // graph BFS from camera 0 and pose chaining (src/mymulticalib.cpp:615-666)
+    virtual void initialize();
+    // reset (src/multicalib.cpp:134-152): clears the edges, the photo vertices and the per-camera
+    // lists (the device copy of the problem is dropped with them)
+    virtual void reset();
+    // writeParameters (src/multicalib.cpp:1092-1127): nCameras, camera_matrix_i,
+    // camera_distortion_i, xi_i (omni), camera_pose_i, meanReprojectError, pose_timestamp_<ts>
+    virtual void writeParameters(const std::string& filename);
 
     // the per-iteration seam (multicalib.hpp:176): deltaX and JTE (P x 1, double) at x;
     // JTJ_inv is left empty (the reference allocates it and never reads it, mymulticalib.cpp:680)
@@ -196,7 +229,7 @@ public:
     }
 
     // drop the device copy of the problem (the next call rebuilds it from the state)
-    void reset() { release(); }
+    void releaseDevice() { release(); }
     int iterations() const { return _iters; }          // Gauss-Newton iterations of the last run
     double lastChange() const { return _change; }      // change = ||G|| / ||x|| of the last update
 
@@ -206,6 +239,21 @@ public:
         _vertexList.emplace_back(pose, timestamp);
         return (int)_vertexList.size() - 1;
     }
+    // getPhotoVertex (src/multicalib.cpp:323-346): the vertex of `timestamp`, created on first use
+    int getPhotoVertex(int timestamp) {
+        for (size_t i = 0; i < _vertexList.size(); ++i)
+            if (_vertexList[i].timestamp == timestamp) {
+                _vertexList[i].timestampCnt++;
+                return (int)i;
+            }
+        _vertexList.emplace_back(eye4(), timestamp);
+        return (int)_vertexList.size() - 1;
+    }
+    // graphTraverse (src/multicalib.cpp:825-851) over the camera-photo graph of _edgeList
+    // (buildGraph, :353-367: the adjacency keeps the LAST edge of a vertex pair); BFS from
+    // `begin`, neighbours in increasing vertex order; pre[v] = -2 (INVALID) when unreached
+    void graphTraverse(int begin, std::vector<int>& order, std::vector<int>& pre,
+                       std::vector<std::vector<std::pair<int, int>>>* adjacency = nullptr) const;
 
     // ---- the state loadImages() + initialize() build (multicalib.hpp:193-214)
     int _camType, _nCamera;
@@ -218,6 +266,12 @@ public:
     std::vector<std::array<float, 9>> _cameraMatrix;                           // row-major 3x3
     std::vector<std::vector<float>> _distortCoeffs;                            // pinhole 4/5/8/12, omni 4
     std::vector<float> _xi;                                                    // Mei xi (omnidirectional)
+    double _error = 0.0;                                                       // meanReprojectError
+    int _verbose = 0;
+    // per camera, per stored view (loadImages): file, timestamp, solvePnP pose
+    std::vector<std::vector<std::string>> filesEachCameraFull;
+    std::vector<std::vector<int>> timestampFull, timestampAvailable;
+    std::vector<std::vector<std::array<float, 3>>> _omEachCamera, _tEachCamera;
 
 protected:
     virtual int model() const { return _camType == OMNIDIRECTIONAL ? MCC_MODEL_OMNI : MCC_MODEL_PINHOLE; }
@@ -287,6 +341,37 @@ public:
     MyMultiCameraCalibration(int nCameras, TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-7),
                              int device = 0)
         : MultiCameraCalibration(PINHOLE, nCameras, criteria, device) {}
+    // the reference constructor (mymulticalib.hpp:91-96, src/mymulticalib.cpp:72-97): reads
+    // <cameraConfigFolder>/<serial>.xml (Intrinsics, Distortion) per camera and, when given, the
+    // double-side transform (key "transform"); corner files are <dataFolder>/<serial>/<ts>.yaml
+    MyMultiCameraCalibration(const std::vector<std::string>& cameraSerials, int cameraType, int nCameras,
+                             const std::string& dataFolder, const std::string& cameraConfigFolder,
+                             const std::string& doubleSideConfig, Size frontPatternSize, Size backPatternSize,
+                             float patternWidth, float patternHeight, int verbose = 0, int showExtration = 0,
+                             int nMiniMatches = 20, int flags = 0,
+                             TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-7),
+                             int device = 0);
+    // loadImages (src/mymulticalib.cpp:349-405): every camera's corner files (sorted), minus
+    // `outliers`; solvePnP per view; views with the front pattern's corner count only
+    // (storeReaded, :237); photo vertices for timestamps seen by >= 2 cameras; one edge per view
+    void loadImages() override { loadImages(std::set<std::string>()); }
+    virtual void loadImages(const std::set<std::string>& outliers);
+    void initialize() override;
+    // removeOutlier (src/mymulticalib.cpp:406-423): drops every edge whose reprojecterror > 0.5
+    // and returns their corner files
+    std::set<std::string> removeOutlier();
+    // writeParameters + writeParameters2config (src/mymulticalib.cpp:424-456): also rewrites each
+    // <cameraConfigFolder>/<serial>.xml with CameraMatrix = the camera's optimised pose
+    void writeParameters(const std::string& filename) override;
+    void reset() override;
+
+    std::vector<std::string> cameraSerials;
+    std::string dataFolder, cameraConfigFolder;
+    Size _FrontPatternSize, _BackPatternSize;
+    std::set<std::string> m_outliers;
+    std::set<int> setOfTimestampIsMulticamera;
+    std::vector<std::vector<bool>> timestampIsMulticamera;
+    int invalidPoseCount = 0;   // views whose solvePnP translation failed isValidPose (dropped)
     std::array<double, 16> doubleSideTransform{};   // CV_64F 4x4; all zero = not loaded
 protected:
     int model() const override { return MCC_MODEL_PINHOLE; }

@@ -48,13 +48,21 @@ class _Desc(ctypes.Structure):
 _LIB = None
 
 
+HOST_LIB_PATH = os.path.join(_HERE, "libmcc_host.so")
+SAMPLE_PATH = os.path.join(_HERE, "build", "multi_cameras_calibration")
+
+
 def build(force: bool = False) -> str:
-    """Compile libmcc.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
-    srcs = [os.path.join(_HERE, "csrc", f) for f in os.listdir(os.path.join(_HERE, "csrc"))]
-    srcs.append(HEADER)
-    stale = not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs)
+    """Compile libmcc.so in-tree for gfx950 (hipcc cross-compiles without a GPU), and the host
+    side of the sample flow (libmcc_host.so, build/multi_cameras_calibration) with g++."""
+    inc = os.path.dirname(HEADER)
+    srcs = [os.path.join(_HERE, d, f) for d in ("csrc", "host", "samples") for f in os.listdir(os.path.join(_HERE, d))]
+    srcs += [os.path.join(inc, f) for f in os.listdir(inc)]
+    outs = [LIB_PATH, HOST_LIB_PATH, SAMPLE_PATH]
+    stale = any(not os.path.exists(o) for o in outs) or any(
+        os.path.getmtime(s) > min(os.path.getmtime(o) for o in outs) for s in srcs)
     if force or stale:
-        subprocess.run(["make", "-C", _HERE, "-j4", "libmcc.so"], check=True)
+        subprocess.run(["make", "-s", "--no-print-directory", "-C", _HERE, "-j4", "all"], check=True)
     return LIB_PATH
 
 

@@ -1,0 +1,392 @@
+// multicalib.cpp -- the reference sample's problem construction and driver around the GPU
+// optimiser (include/mcc_multicalib.hpp):
+//   MyMultiCameraCalibration(...)   src/mymulticalib.cpp:72-131  (camera configs, double side)
+//   loadImages(outliers)            src/mymulticalib.cpp:182-405 (corner files, solvePnP, filter)
+//   initialize()                    src/mymulticalib.cpp:615-666 (graph BFS pose chaining)
+//   removeOutlier()                 src/mymulticalib.cpp:406-423
+//   reset() / run()                 src/multicalib.cpp:127-152
+//   writeParameters(...)            src/multicalib.cpp:1092-1127, src/mymulticalib.cpp:424-456
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <filesystem>
+#include <iostream>
+
+#include "mcc_multicalib.hpp"
+#include "mcc_pnp.hpp"
+#include "mcc_storage.hpp"
+
+namespace mcc {
+namespace multicalib {
+
+namespace {
+
+namespace stg = mcc::storage;
+constexpr int INVALID = -2;
+
+// pose algebra in double, results rounded to the reference's CV_32F poses
+void to_d(const Pose& P, double* D) {
+    for (int k = 0; k < 16; ++k) D[k] = P[k];
+}
+Pose to_f(const double* D) {
+    Pose P;
+    for (int k = 0; k < 16; ++k) P[k] = (float)D[k];
+    return P;
+}
+void mul4(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 4; ++k) s += A[4 * i + k] * B[4 * k + j];
+            C[4 * i + j] = s;
+        }
+}
+// Mat::inv of a 4 x 4 (Gauss-Jordan with partial pivoting, as DECOMP_LU would)
+void inv4(const double* A, double* X) {
+    double M[4][8];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) M[i][j] = j < 4 ? A[4 * i + j] : (j - 4 == i ? 1.0 : 0.0);
+    for (int k = 0; k < 4; ++k) {
+        int p = k;
+        for (int i = k + 1; i < 4; ++i)
+            if (std::fabs(M[i][k]) > std::fabs(M[p][k])) p = i;
+        if (M[p][k] == 0.0) throw std::runtime_error("singular pose in initialize()");
+        if (p != k)
+            for (int j = 0; j < 8; ++j) std::swap(M[k][j], M[p][j]);
+        const double d = M[k][k];
+        for (int j = 0; j < 8; ++j) M[k][j] /= d;
+        for (int i = 0; i < 4; ++i) {
+            if (i == k) continue;
+            const double f = M[i][k];
+            for (int j = 0; j < 8; ++j) M[i][j] -= f * M[k][j];
+        }
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) X[4 * i + j] = M[i][4 + j];
+}
+
+stg::Mat pose_mat(const Pose& P) {
+    stg::Mat m(4, 4, 'f');
+    for (int k = 0; k < 16; ++k) m.data[k] = P[k];
+    return m;
+}
+
+// cv::Mat -> flat values of a points matrix: N x k (1 channel) or N x 1 (k channels)
+std::vector<double> points_of(const stg::Node& n, int k, const std::string& file, const char* key) {
+    if (n.type != stg::Node::MAT) throw std::runtime_error(file + ": no matrix '" + key + "'");
+    const stg::Mat& m = n.mat;
+    if ((m.cols * m.channels) % k != 0 && (m.rows * m.cols * m.channels) % k != 0)
+        throw std::runtime_error(file + ": '" + key + "' is not a list of " + std::to_string(k) + "-vectors");
+    return m.data;
+}
+
+bool is_valid_pose(const float t[3]) {   // isValidPose (src/multicalib.cpp:104-126): 300 < |t| < 3000 mm
+    const float r = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+    return r < 3000.f && r > 300.f;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- base class
+double MultiCameraCalibration::run() {
+    loadImages();
+    initialize();
+    return optimizeExtrinsics();
+}
+
+void MultiCameraCalibration::loadImages() {
+    throw std::runtime_error(
+        "MultiCameraCalibration::loadImages: random-pattern feature matching on images is out of scope; use "
+        "MyMultiCameraCalibration (pre-detected corner files) or fill the state directly");
+}
+
+void MultiCameraCalibration::graphTraverse(int begin, std::vector<int>& order, std::vector<int>& pre,
+                                           std::vector<std::vector<std::pair<int, int>>>* adjacency) const {
+    const int nV = (int)_vertexList.size();
+    // buildGraph: G(c, p) = G(p, c) = edgeIdx + 1, a later edge of the same pair overwrites
+    std::vector<std::vector<std::pair<int, int>>> adj(nV);
+    auto link = [&](int a, int b, int e) {
+        for (auto& q : adj[a])
+            if (q.first == b) {
+                q.second = e;
+                return;
+            }
+        adj[a].push_back({b, e});
+    };
+    for (int e = 0; e < (int)_edgeList.size(); ++e) {
+        const int c = _edgeList[e].cameraVertex, p = _edgeList[e].photoVertex;
+        if (c < 0 || c >= nV || p < 0 || p >= nV) throw std::runtime_error("edge refers to a missing vertex");
+        link(c, p, e);
+        link(p, c, e);
+    }
+    for (auto& a : adj) std::sort(a.begin(), a.end());   // findRowNonZero: increasing index
+    order.clear();
+    pre.assign(nV, INVALID);
+    if (begin < 0 || begin >= nV) throw std::runtime_error("graphTraverse: bad start vertex");
+    std::vector<char> visited(nV, 0);
+    std::vector<int> queue{begin};
+    visited[begin] = 1;
+    pre[begin] = -1;
+    order.push_back(begin);
+    for (size_t h = 0; h < queue.size(); ++h) {
+        const int v = queue[h];
+        for (const auto& q : adj[v])
+            if (!visited[q.first]) {
+                visited[q.first] = 1;
+                queue.push_back(q.first);
+                order.push_back(q.first);
+                pre[q.first] = v;
+            }
+    }
+    if (adjacency) *adjacency = std::move(adj);
+}
+
+void MultiCameraCalibration::initialize() {
+    std::vector<int> order, pre;
+    std::vector<std::vector<std::pair<int, int>>> adj;
+    graphTraverse(0, order, pre, &adj);
+    for (int i = 0; i < _nCamera; ++i)
+        if (pre[i] == INVALID) std::cout << "camera" << i << "is not connected" << std::endl;
+    const double* dsInv = nullptr;
+    double dsi[16];
+    if (auto* my = dynamic_cast<MyMultiCameraCalibration*>(this)) {
+        bool any = false;
+        for (double v : my->doubleSideTransform) any = any || v != 0.0;
+        if (any) {
+            inv4(my->doubleSideTransform.data(), dsi);
+            dsInv = dsi;
+        }
+    }
+    for (size_t i = 1; i < order.size(); ++i) {
+        const int v = order[i], pv = pre[v];
+        int e = -1;
+        for (const auto& q : adj[v])
+            if (q.first == pv) e = q.second;
+        const edge& eg = _edgeList[e];
+        double prePose[16], preInv[16], T[16], out[16];
+        to_d(_vertexList[pv].pose, prePose);
+        inv4(prePose, preInv);
+        to_d(eg.transform, T);
+        if (eg.patternSide == BACK_PATTERN) {   // front pose = back pose * doubleSideTransform^-1
+            if (!dsInv) throw std::runtime_error("BACK edge without doubleSideTransform");
+            double t2[16];
+            mul4(T, dsInv, t2);
+            std::copy(t2, t2 + 16, T);
+        }
+        if (v < _nCamera) mul4(T, preInv, out);    // camera: transform * prePose^-1
+        else mul4(preInv, T, out);                 // photo:  prePose^-1 * transform
+        _vertexList[v].pose = to_f(out);
+        if (_verbose && v < _nCamera) std::cout << "initial pose for camera " << v << " set" << std::endl;
+    }
+    release();
+}
+
+void MultiCameraCalibration::reset() {
+    _edgeList.clear();
+    _vertexList.clear();
+    for (int i = 0; i < _nCamera; ++i) _vertexList.emplace_back();
+    for (int i = 0; i < _nCamera; ++i) {
+        filesEachCameraFull[i].clear();
+        timestampFull[i].clear();
+        timestampAvailable[i].clear();
+        _objectPointsForEachCamera[i].clear();
+        _imagePointsForEachCamera[i].clear();
+        _omEachCamera[i].clear();
+        _tEachCamera[i].clear();
+    }
+    release();
+}
+
+void MultiCameraCalibration::writeParameters(const std::string& filename) {
+    stg::FileStorage fs(filename, stg::FileStorage::WRITE);
+    if (!fs.isOpened()) throw std::runtime_error("cannot open " + filename + " for writing");
+    fs.write("nCameras", _nCamera);
+    for (int c = 0; c < _nCamera; ++c) {
+        const std::string i = std::to_string(c);
+        stg::Mat K(3, 3, 'f');
+        for (int k = 0; k < 9; ++k) K.data[k] = _cameraMatrix[c][k];
+        stg::Mat D(1, (int)_distortCoeffs[c].size(), 'f');
+        for (size_t k = 0; k < _distortCoeffs[c].size(); ++k) D.data[k] = _distortCoeffs[c][k];
+        fs.write("camera_matrix_" + i, K);
+        fs.write("camera_distortion_" + i, D);
+        if (_camType == OMNIDIRECTIONAL) fs.write("xi_" + i, (double)_xi[c]);
+        fs.write("camera_pose_" + i, pose_mat(_vertexList[c].pose));
+    }
+    fs.write("meanReprojectError", _error);
+    for (size_t v = _nCamera; v < _vertexList.size(); ++v)
+        fs.write("pose_timestamp_" + std::to_string(_vertexList[v].timestamp), pose_mat(_vertexList[v].pose));
+    fs.release();
+}
+
+// ---------------------------------------------------------------- MyMultiCameraCalibration
+MyMultiCameraCalibration::MyMultiCameraCalibration(const std::vector<std::string>& serials, int cameraType,
+                                                   int nCameras, const std::string& dataFolder_,
+                                                   const std::string& cameraConfigFolder_,
+                                                   const std::string& doubleSideConfig, Size frontPatternSize,
+                                                   Size backPatternSize, float, float, int verbose, int, int, int,
+                                                   TermCriteria criteria, int device)
+    : MultiCameraCalibration(cameraType, nCameras, criteria, device), cameraSerials(serials), dataFolder(dataFolder_),
+      cameraConfigFolder(cameraConfigFolder_), _FrontPatternSize(frontPatternSize), _BackPatternSize(backPatternSize),
+      timestampIsMulticamera(nCameras) {
+    if ((int)serials.size() != nCameras) throw std::runtime_error("one camera serial per camera is required");
+    _verbose = verbose;
+    // readcameraIntrinsics (src/mymulticalib.cpp:118-131)
+    for (int c = 0; c < nCameras; ++c) {
+        const std::string fn = cameraConfigFolder + "/" + serials[c] + ".xml";
+        stg::FileStorage fs(fn, stg::FileStorage::READ);
+        if (!fs.isOpened()) throw std::runtime_error("cannot read camera config " + fn);
+        const stg::Node& K = fs["Intrinsics"];
+        const stg::Node& D = fs["Distortion"];
+        if (K.type != stg::Node::MAT || K.mat.data.size() != 9) throw std::runtime_error(fn + ": Intrinsics must be 3x3");
+        if (D.type != stg::Node::MAT) throw std::runtime_error(fn + ": no Distortion");
+        for (int k = 0; k < 9; ++k) _cameraMatrix[c][k] = (float)K.mat.data[k];
+        _distortCoeffs[c].assign(D.mat.data.begin(), D.mat.data.end());
+    }
+    // readDoubleSide (src/mymulticalib.cpp:99-103)
+    if (!doubleSideConfig.empty()) {
+        stg::FileStorage fs(doubleSideConfig, stg::FileStorage::READ);
+        if (!fs.isOpened()) throw std::runtime_error("cannot read " + doubleSideConfig);
+        const stg::Node& T = fs["transform"];
+        if (T.type != stg::Node::MAT || T.mat.data.size() != 16)
+            throw std::runtime_error(doubleSideConfig + ": transform must be 4x4");
+        std::copy(T.mat.data.begin(), T.mat.data.end(), doubleSideTransform.begin());
+    }
+}
+
+void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers) {
+    namespace fsys = std::filesystem;
+    if (!outliers.empty()) m_outliers = outliers;
+    const int frontN = _FrontPatternSize.width * _FrontPatternSize.height;
+    const int backN = _BackPatternSize.width * _BackPatternSize.height;
+    for (int cam = 0; cam < _nCamera; ++cam) {   // loadOneSerial (src/mymulticalib.cpp:262-301)
+        const std::string folder = dataFolder + "/" + cameraSerials[cam];
+        std::vector<std::string> files;
+        if (fsys::is_directory(folder))
+            for (const auto& de : fsys::directory_iterator(folder))
+                if (de.path().extension() == ".yaml") files.push_back(de.path().string());
+        std::sort(files.begin(), files.end());   // cv::glob returns sorted paths
+        double K[9];
+        for (int k = 0; k < 9; ++k) K[k] = _cameraMatrix[cam][k];
+        const std::vector<double> D(_distortCoeffs[cam].begin(), _distortCoeffs[cam].end());
+        for (const std::string& file : files) {
+            if (m_outliers.count(file)) {
+                std::cout << "outlier:" << file << " skipped: " << std::endl;
+                continue;
+            }
+            const int timestamp = std::stoi(fsys::path(file).stem().string());   // readTimestamps
+            stg::FileStorage fs(file, stg::FileStorage::READ);                    // readCorners
+            if (!fs.isOpened()) throw std::runtime_error("cannot read " + file);
+            const std::vector<double> img = points_of(fs["corners"], 2, file, "corners");
+            const std::vector<double> objd = points_of(fs["objects"], 3, file, "objects");
+            const int n = (int)img.size() / 2;
+            if ((int)objd.size() != 3 * n) throw std::runtime_error(file + ": corners and objects differ in count");
+            std::vector<double> obj(objd.size());   // objectPoints.convertTo(CV_32F)
+            for (size_t k = 0; k < objd.size(); ++k) obj[k] = (double)(float)objd[k];
+            double r[3], t[3];   // calcPatternPose: cv::solvePnP
+            if (mcc::pnp::solvePnP(obj.data(), img.data(), n, K, D, r, t) < 0)
+                throw std::runtime_error(file + ": too few corners for solvePnP");
+            const std::array<float, 3> om{(float)r[0], (float)r[1], (float)r[2]};
+            const std::array<float, 3> tv{(float)t[0], (float)t[1], (float)t[2]};
+            if (!is_valid_pose(tv.data())) {   // the reference asserts (a no-op in release builds)
+                ++invalidPoseCount;
+                std::cout << "invalid pattern :" << invalidPoseCount << ", " << file << std::endl;
+                continue;
+            }
+            if (n != frontN) continue;   // storeReaded: front-pattern views only (src/mymulticalib.cpp:237)
+            filesEachCameraFull[cam].push_back(file);
+            timestampFull[cam].push_back(timestamp);
+            timestampAvailable[cam].push_back(timestamp);
+            _omEachCamera[cam].push_back(om);
+            _tEachCamera[cam].push_back(tv);
+            std::vector<float> fi(img.size()), fo(obj.size());
+            for (size_t k = 0; k < img.size(); ++k) fi[k] = (float)img[k];
+            for (size_t k = 0; k < obj.size(); ++k) fo[k] = (float)obj[k];
+            _imagePointsForEachCamera[cam].push_back(std::move(fi));
+            _objectPointsForEachCamera[cam].push_back(std::move(fo));
+        }
+    }
+    // identifyMultiCameraTimestamps (src/mymulticalib.cpp:314-347)
+    setOfTimestampIsMulticamera.clear();
+    for (int cam = 0; cam < _nCamera; ++cam) {
+        timestampIsMulticamera[cam].clear();
+        for (int ts : timestampAvailable[cam]) {
+            bool found = false;
+            for (int c2 = 0; c2 < _nCamera && !found; ++c2)
+                if (c2 != cam)
+                    found = std::find(timestampAvailable[c2].begin(), timestampAvailable[c2].end(), ts) !=
+                            timestampAvailable[c2].end();
+            timestampIsMulticamera[cam].push_back(found);
+            if (found) setOfTimestampIsMulticamera.insert(ts);
+        }
+    }
+    // edges (src/mymulticalib.cpp:362-403)
+    for (int cam = 0; cam < _nCamera; ++cam)
+        for (int i = 0; i < (int)_omEachCamera[cam].size(); ++i) {
+            const int ts = timestampAvailable[cam][i];
+            if (!setOfTimestampIsMulticamera.count(ts)) continue;
+            const int pv = getPhotoVertex(ts);
+            Pose T = rt_to_pose(_omEachCamera[cam][i].data(), _tEachCamera[cam][i].data());
+            edge eg(cam, pv, i, T);
+            if ((int)_imagePointsForEachCamera[cam][i].size() / 2 == backN) eg.patternSide = BACK_PATTERN;
+            _edgeList.push_back(eg);
+        }
+    release();
+}
+
+void MyMultiCameraCalibration::initialize() { MultiCameraCalibration::initialize(); }
+
+std::set<std::string> MyMultiCameraCalibration::removeOutlier() {
+    std::vector<edge> kept;
+    std::set<std::string> names;
+    int cnt = 0;
+    for (const edge& eg : _edgeList) {
+        if (eg.reprojecterror > 0.5f) {
+            const std::string& f = filesEachCameraFull[eg.cameraVertex][eg.photoIndex];
+            std::cout << "outlier:" << eg.reprojecterror << ":" << f << " removed" << std::endl;
+            names.insert(f);
+            ++cnt;
+        } else {
+            kept.push_back(eg);
+        }
+    }
+    std::cout << "Totally " << cnt << " outlier removed" << std::endl;
+    _edgeList = kept;
+    release();
+    return names;
+}
+
+void MyMultiCameraCalibration::reset() {
+    MultiCameraCalibration::reset();
+    for (auto& v : timestampIsMulticamera) v.clear();
+    setOfTimestampIsMulticamera.clear();
+}
+
+void MyMultiCameraCalibration::writeParameters(const std::string& filename) {
+    MultiCameraCalibration::writeParameters(filename);
+    // writeParameters2config (src/mymulticalib.cpp:424-449): rewrite each camera config with
+    // CameraMatrix = the camera's optimised pose
+    const char* scalarNames[2] = {"depth_scale", "height"};
+    const char* matNames[3] = {"CameraMatrix", "Intrinsics", "Distortion"};
+    for (int c = 0; c < _nCamera; ++c) {
+        const std::string fn = cameraConfigFolder + "/" + cameraSerials[c] + ".xml";
+        double scalars[2] = {0.0, 0.0};
+        stg::Mat mats[3];
+        {
+            stg::FileStorage in(fn, stg::FileStorage::READ);
+            if (!in.isOpened()) throw std::runtime_error("cannot read camera config " + fn);
+            for (int i = 0; i < 2; ++i)
+                if (!in[scalarNames[i]].empty()) scalars[i] = in[scalarNames[i]].toReal();
+            for (int i = 0; i < 3; ++i)
+                if (in[matNames[i]].type == stg::Node::MAT) mats[i] = in[matNames[i]].mat;
+        }
+        mats[0] = pose_mat(_vertexList[c].pose);
+        stg::FileStorage out(fn, stg::FileStorage::WRITE);
+        for (int i = 0; i < 2; ++i) out.write(scalarNames[i], (double)(float)scalars[i]);
+        for (int i = 0; i < 3; ++i)
+            if (!mats[i].empty()) out.write(matNames[i], mats[i]);
+        out.release();
+    }
+}
+
+}  // namespace multicalib
+}  // namespace mcc

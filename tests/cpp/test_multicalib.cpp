@@ -6,12 +6,16 @@
 //                                         buildParas / paras2vertex layouts, error behaviour
 //   test_multicalib run <in.bin> <out.txt>  fixture problem (written by the test from a golden
 //                                         npz): seam at x0, computeProjectError, optimizeExtrinsics
+//   test_multicalib storage <file>        FileStorage read: one line per top-level key
+//                                         (kind, rows x cols x channels / sequence length)
 //
 // The input blob: int32 header [magic, model, C, V, E, nd, corners, has_ds, has_campose,
 // crit_type, crit_max], float64 eps, then edge_cam, edge_photo, edge_side, edge_off, edge_n
 // (int32 [E]), obj [3 corners], img [2 corners], K [9C], D [nd C], xi [C] (float32),
 // ds_pose [16] float64 (if has_ds), cam_pose [16 C] float32 (if has_campose), x0 [P] float32.
 #include "mcc_multicalib.hpp"
+#include "mcc_pnp.hpp"
+#include "mcc_storage.hpp"
 
 #include <cstdio>
 #include <cstring>
@@ -113,6 +117,56 @@ static int selftest() {
         MyMultiCameraCalibration mc3(1);                             // edge to a missing photo slot
         mc3._edgeList.emplace_back(0, 1, 5, eye4());
         EXPECT(throws([&] { mc3.optimizeExtrinsics(); }));
+    }
+    // solvePnP (cv::solvePnP restated): exact synthetic views, planar and non-planar, with
+    // Brown-Conrady and rational distortion, recover the pose
+    {
+        const double K[9] = {1200, 0, 960, 0, 1180, 540, 0, 0, 1};
+        const std::vector<std::vector<double>> Ds = {{-0.1, 0.05, 1e-4, -2e-4, 0.0}, {-0.12, 0.08, 2e-4, 1e-4, 0.01, 0.002, -0.001, 0.003}};
+        for (const auto& D : Ds)
+            for (int planar = 0; planar < 2; ++planar) {
+                std::vector<double> obj;
+                for (int i = 0; i < 8; ++i)
+                    for (int j = 0; j < 11; ++j)
+                        obj.insert(obj.end(), {40.0 * j, 40.0 * i, planar ? 0.0 : 15.0 * std::sin(0.7 * i + 0.3 * j)});
+                const int n = (int)obj.size() / 3;
+                const double r[3] = {0.3, -0.4, 0.2}, t[3] = {-150.0, -90.0, 1300.0};
+                std::vector<double> img(2 * n);
+                mcc::pnp::projectPoints(obj.data(), n, r, t, K, D, img.data());
+                double rr[3], tt[3];
+                const double rms = mcc::pnp::solvePnP(obj.data(), img.data(), n, K, D, rr, tt);
+                EXPECT(rms >= 0 && rms < 1e-6);
+                for (int k = 0; k < 3; ++k) {
+                    EXPECT(std::fabs(rr[k] - r[k]) < 1e-7);
+                    EXPECT(std::fabs(tt[k] - t[k]) < 1e-4);
+                }
+            }
+    }
+    // FileStorage: write XML and YAML, read back every kind
+    for (const char* ext : {".xml", ".yaml"}) {
+        const std::string fn = std::string("/tmp/mcc_storage_selftest") + ext;
+        {
+            mcc::storage::FileStorage fs(fn, mcc::storage::FileStorage::WRITE);
+            fs.write("nCameras", 3);
+            fs.write("meanReprojectError", 0.123456789012345);
+            fs.write("name", std::string("rig"));
+            mcc::storage::Mat m(2, 3, 'd');
+            for (int k = 0; k < 6; ++k) m.data[k] = 0.1 * k - 0.25;
+            fs.write("M", m);
+            mcc::storage::Mat pts(4, 1, 'f', 2);
+            for (int k = 0; k < 8; ++k) pts.data[k] = (double)(float)(1.5f * k + 0.3f);
+            fs.write("pts", pts);
+        }
+        mcc::storage::FileStorage in(fn, mcc::storage::FileStorage::READ);
+        EXPECT(in.isOpened());
+        EXPECT(in["nCameras"].toInt() == 3);
+        EXPECT(std::fabs(in["meanReprojectError"].toReal() - 0.123456789012345) < 1e-15);
+        EXPECT(in["name"].str == "rig");
+        EXPECT(in["M"].type == mcc::storage::Node::MAT && in["M"].mat.rows == 2 && in["M"].mat.cols == 3);
+        EXPECT(in["M"].mat.data[5] == 0.1 * 5 - 0.25);
+        EXPECT(in["pts"].mat.channels == 2 && in["pts"].mat.depth == 'f' && in["pts"].mat.data[7] == (double)(float)(1.5f * 7 + 0.3f));
+        EXPECT(in["missing"].empty());
+        EXPECT(in.keys().size() == 5);
     }
     std::printf("selftest %s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
     return g_fail ? 1 : 0;
@@ -221,6 +275,21 @@ int main(int argc, char** argv) {
     try {
         if (argc >= 2 && !std::strcmp(argv[1], "selftest")) return selftest();
         if (argc >= 4 && !std::strcmp(argv[1], "run")) return run(argv[2], argv[3]);
+        if (argc >= 3 && !std::strcmp(argv[1], "storage")) {
+            mcc::storage::FileStorage fs(argv[2], mcc::storage::FileStorage::READ);
+            if (!fs.isOpened()) throw std::runtime_error("cannot open");
+            for (const std::string& k : fs.keys()) {
+                const mcc::storage::Node& n = fs[k];
+                if (n.type == mcc::storage::Node::MAT)
+                    std::printf("%s mat %d %d %d\n", k.c_str(), n.mat.rows, n.mat.cols, n.mat.channels);
+                else if (n.type == mcc::storage::Node::SEQ)
+                    std::printf("%s seq %zu %s\n", k.c_str(), n.seq.size(),
+                                n.seq.empty() ? "-" : (n.seq[0].type == mcc::storage::Node::MAT ? "mat" : "scalar"));
+                else
+                    std::printf("%s scalar\n", k.c_str());
+            }
+            return 0;
+        }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 2;

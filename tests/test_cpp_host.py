@@ -31,7 +31,7 @@ def exe(tmp_path_factory):
     libdir = os.path.dirname(api.LIB_PATH)
     out = str(tmp_path_factory.mktemp("cpp") / "test_multicalib")
     subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    SRC, "-L", libdir, "-lmcc", f"-Wl,-rpath,{libdir}", "-o", out], check=True)
+                    SRC, "-L", libdir, "-lmcc_host", "-lmcc", f"-Wl,-rpath,{libdir}", "-o", out], check=True)
     return out
 
 

@@ -1,0 +1,176 @@
+"""The reference sample's flow on this build: MyMultiCameraCalibration
+over corner files -> loadImages (solvePnP init, multi-camera filter) -> initialize (graph BFS) ->
+optimizeExtrinsics (GPU) -> removeOutlier -> reset -> loadImages(outliers) -> initialize ->
+optimizeExtrinsics -> writeParameters (samples/multi_cameras_calibration.cpp:46-83).
+
+Driven through multi_camera_calibration_amd/build/multi_cameras_calibration on a synthetic rig
+written in the reference's on-disk layout (tests/sample_data.py; the reference's own corner data
+is not in its repository).
+
+CPU: the loaded problem (edges in camera-major file order, photo vertices in first-appearance
+order, points, the 88-corner front filter) equals the rig's; the solvePnP + BFS initial poses are
+close to the truth; the FileStorage reader parses the reference's tutorial XML.
+GPU: outliers found are exactly the corrupted files; the pass-2 optimisation equals the oracle
+run on the sample's own problem and initial vector; the written XML results and rewritten camera
+configs carry the optimised poses.
+"""
+import os
+import subprocess
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from multi_camera_calibration_amd import api, rig
+from oracle import oracle_py as O
+
+import sample_data as SD
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TUTORIAL = "/root/reference/tutorials/data"
+
+
+@pytest.fixture(scope="module")
+def sample():
+    api.build()
+    return api.SAMPLE_PATH
+
+
+def _rig():
+    return rig.make_rig(n_cams=3, n_views=40, seed=11, visibility=0.7)
+
+
+def _run(sample, args, timeout=300):
+    r = subprocess.run([sample] + args, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return r.stdout
+
+
+def _rot(rv):
+    rv = np.asarray(rv, np.float64)
+    th = np.linalg.norm(rv)
+    if th < 1e-300:
+        return np.eye(3)
+    k = rv / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def test_storage_reads_reference_tutorial_data(tmp_path):
+    if not os.path.isdir(TUTORIAL):
+        pytest.skip("reference tutorial data not present")
+    api.build()
+    exe = str(tmp_path / "t")
+    libdir = os.path.dirname(api.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "test_multicalib.cpp"), "-L", libdir, "-lmcc_host", "-lmcc",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    out = subprocess.run([exe, "storage", os.path.join(TUTORIAL, "omni_calib_data.xml")], capture_output=True,
+                         text=True, check=True).stdout.split("\n")
+    assert "objectPoints seq 15 mat" in out and "imagePoints seq 15 mat" in out and "imageSize seq 2 scalar" in out
+    out = subprocess.run([exe, "storage", os.path.join(TUTORIAL, "omni_stereocalib_data.xml")], capture_output=True,
+                         text=True, check=True).stdout.split("\n")
+    assert "objectPoints seq 39 mat" in out and "imagePoints2 seq 39 mat" in out
+
+
+def _expected_order(p, stamps, skip_edges=()):
+    """Edges as loadImages builds them: per camera, its views in file (timestamp) order; photo
+    vertices in order of first appearance (getPhotoVertex)."""
+    skip = set(int(e) for e in skip_edges)
+    edges = []
+    for c in range(p.n_cams):
+        es = [int(e) for e in np.nonzero(p.edge_cam == c)[0] if int(e) not in skip]
+        es.sort(key=lambda e: stamps[int(p.edge_photo[e])])
+        edges += es
+    # the multi-camera filter: timestamps seen by >= 2 cameras among the kept views
+    cnt = {}
+    for e in edges:
+        cnt[int(p.edge_photo[e])] = cnt.get(int(p.edge_photo[e]), 0) + 1
+    edges = [e for e in edges if cnt[int(p.edge_photo[e])] >= 2]
+    photos = []
+    for e in edges:
+        ph = int(p.edge_photo[e])
+        if ph not in photos:
+            photos.append(ph)
+    return edges, photos
+
+
+def test_sample_load_initialize_cpu(sample, tmp_path):
+    p = _rig()
+    outl = [3, 17, 40]
+    serials, data, config, files, stamps = SD.write_dataset(p, str(tmp_path), outlier_edges=outl, back_views=2)
+    dump = str(tmp_path / "problem.bin")
+    _run(sample, ["--serials", ",".join(serials), "--data", data, "--config", config, "--init-only",
+                  "--dump-problem", dump])
+    q, ts = SD.read_dump(dump)
+    edges, photos = _expected_order(p, stamps)
+    assert q.n_edges == len(edges) and q.n_photos == len(photos)   # back views (70 corners) dropped
+    assert list(ts) == [int(stamps[ph]) for ph in photos]
+    for k, e in enumerate(edges):
+        assert int(q.edge_cam[k]) == int(p.edge_cam[e])
+        assert photos[int(q.edge_photo[k])] == int(p.edge_photo[e])
+        o, n = int(p.edge_off[e]), int(p.edge_n[e])
+        qo = int(q.edge_off[k])
+        assert np.array_equal(q.obj[qo:qo + n], p.obj[o:o + n])
+        shift = SD.outlier_noise(e, n, 2.0) if e in outl else 0.0
+        assert np.array_equal(q.img[qo:qo + n], (p.img[o:o + n].astype(np.float64) + shift).astype(np.float32))
+    # solvePnP + BFS chaining: initial poses near the truth (0.2 px noise, outliers 2 px, errors
+    # accumulate along the chain; solvePnP itself is pinned on exact data by the C++ selftest)
+    m = 6 * (p.n_cams - 1)
+    for c in range(1, p.n_cams):
+        xq, xt = q.x0[6 * (c - 1):6 * c], p.x_true[6 * (c - 1):6 * c]
+        assert np.abs(_rot(xq[:3]) - _rot(xt[:3])).max() < 1e-2
+        assert np.abs(xq[3:] - xt[3:]).max() < 20.0
+    for k, ph in enumerate(photos):
+        xq, xt = q.x0[m + 6 * k:m + 6 * k + 6], p.x_true[p.photo_col(ph):p.photo_col(ph) + 6]
+        assert np.abs(_rot(xq[:3]) - _rot(xt[:3])).max() < 1e-2
+        assert np.abs(xq[3:] - xt[3:]).max() < 20.0
+
+
+def _xml_mat(root, key):
+    e = root.find(key)
+    rows, cols = int(e.find("rows").text), int(e.find("cols").text)
+    return np.array([float(v) for v in e.find("data").text.split()]).reshape(rows, cols)
+
+
+@pytest.mark.gpu
+def test_sample_two_pass_flow(sample, tmp_path):
+    p = _rig()
+    outl = [3, 17, 40]
+    serials, data, config, files, stamps = SD.write_dataset(p, str(tmp_path), outlier_edges=outl, back_views=2)
+    dump, res, out = str(tmp_path / "problem.bin"), str(tmp_path / "result.txt"), str(tmp_path / "results.xml")
+    _run(sample, ["--serials", ",".join(serials), "--data", data, "--config", config, "--out", out,
+                  "--dump-problem", dump, "--dump-result", res])
+    r = SD.read_result(res)
+    # pass 1 finds exactly the corrupted views (per-edge mean error > 0.5 px)
+    assert sorted(r["outliers"]) == sorted(fn for fn, e in files.items() if e in outl)
+    # pass 2: the sample's own problem and initial vector through the oracle
+    q, ts = SD.read_dump(dump)
+    edges, photos = _expected_order(p, stamps, skip_edges=outl)
+    assert q.n_edges == len(edges)
+    crit = (3, 200, 1e-7)
+    x_ref, m_ref, it_ref, _ = O.Oracle(q).optimize(q.x0, *crit)
+    assert r["iterations"] == it_ref
+    assert abs(r["error"] - m_ref) <= 1e-6
+    xo = r["x"].astype(np.float64).reshape(-1, 6)
+    xr = np.asarray(x_ref, np.float64).reshape(-1, 6)
+    for a, b in zip(xo, xr):   # as poses (buildParas' matrix -> vector step may flip near pi)
+        assert np.abs(_rot(a[:3]) - _rot(b[:3])).max() <= 1e-3
+    assert np.abs(xo[:, 3:] - xr[:, 3:]).max() <= 1e-4 * np.abs(xr[:, 3:]).max()
+    # writeParameters: the reference's keys and the optimised poses
+    root = ET.parse(out).getroot()
+    assert int(root.find("nCameras").text) == 3
+    assert abs(float(root.find("meanReprojectError").text) - r["error"]) <= 1e-12 * max(1.0, r["error"])
+    assert np.allclose(_xml_mat(root, "camera_pose_0"), np.eye(4))
+    for c in range(1, 3):
+        P = _xml_mat(root, f"camera_pose_{c}")
+        assert np.abs(P[:3, :3] - _rot(xo[c - 1, :3])).max() <= 1e-5   # float Rodrigues round trips
+        assert np.abs(P[:3, 3] - xo[c - 1, 3:]).max() <= 1e-3
+        assert np.allclose(_xml_mat(root, f"camera_matrix_{c}"), p.K[c], rtol=1e-6)
+    assert sum(1 for e in root if e.tag.startswith("pose_timestamp_")) == q.n_photos
+    # writeParameters2config: each camera config rewritten with CameraMatrix = its pose
+    for c, s in enumerate(serials):
+        croot = ET.parse(os.path.join(config, s + ".xml")).getroot()
+        assert np.allclose(_xml_mat(croot, "CameraMatrix"), _xml_mat(root, f"camera_pose_{c}"))
+        assert np.allclose(_xml_mat(croot, "Intrinsics"), p.K[c], rtol=1e-6)
+        assert croot.find("depth_scale") is not None and croot.find("height") is not None
