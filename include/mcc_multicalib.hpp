@@ -254,6 +254,8 @@ public:
     // `begin`, neighbours in increasing vertex order; pre[v] = -2 (INVALID) when unreached
     void graphTraverse(int begin, std::vector<int>& order, std::vector<int>& pre,
                        std::vector<std::vector<std::pair<int, int>>>* adjacency = nullptr) const;
+    // initialize's pose chaining along the BFS tree (setCameras = false: fixed cameras)
+    void chainPoses(bool setCameras);
 
     // ---- the state loadImages() + initialize() build (multicalib.hpp:193-214)
     int _camType, _nCamera;
@@ -373,6 +375,18 @@ public:
     std::vector<std::vector<bool>> timestampIsMulticamera;
     int invalidPoseCount = 0;   // views whose solvePnP translation failed isValidPose (dropped)
     std::array<double, 16> doubleSideTransform{};   // CV_64F 4x4; all zero = not loaded
+
+protected:
+    // storeReaded (src/mymulticalib.cpp:233-239): front-pattern views only
+    virtual bool keepView(int nCorners) const { return nCorners == _FrontPatternSize.width * _FrontPatternSize.height; }
+    // findTimStamp (src/mymulticalib.cpp:303-312): another camera saw the timestamp at all
+    virtual bool sameTimestampMatches(int nCorners, int nCornersOther) const {
+        (void)nCorners;
+        (void)nCornersOther;
+        return true;
+    }
+
+public:
 protected:
     int model() const override { return MCC_MODEL_PINHOLE; }
     void extraDesc(mcc_desc& d) override {
@@ -389,6 +403,23 @@ public:
     DoubleSideCalibration(int nCameras, TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-8),
                           int device = 0)
         : MyMultiCameraCalibration(nCameras, criteria, device), camerasPose(nCameras, eye4()) {}
+    // the reference constructor (doubleSide.hpp:99-105, src/doubleSide.cpp:6-26): intrinsics as
+    // MyMulti, fixed camera poses from each config's "CameraMatrix" (loadCameraPose, :276-287)
+    DoubleSideCalibration(const std::vector<std::string>& cameraSerials, int cameraType, int nCameras,
+                          const std::string& dataFolder, const std::string& cameraConfigFolder, Size frontPatternSize,
+                          Size backPatternSize, float patternWidth, float patternHeight, int verbose = 0,
+                          int showExtration = 0, int nMiniMatches = 20, int flags = 0,
+                          TermCriteria criteria = TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-8),
+                          int device = 0);
+    // initializeDoublesideTransform (src/doubleSide.cpp:119-165) from the first photo seen on both
+    // sides, then the photo poses by the graph BFS (cameras stay fixed; :167-231).  Generalised
+    // past the reference's two-camera limit (it asserts exactly two edges for that photo and does
+    // not order them): the photo's first FRONT and first BACK edge are used.
+    void initialize() override;
+    // writeDoubleSideTransform (src/doubleSide.cpp:582-590): "doublesideTransform.yaml" in the
+    // working directory, key "transform" (the reference writes nothing else)
+    void writeParameters(const std::string& filename) override;
+    void reset() override;
     std::vector<Pose> camerasPose;      // doubleSide.hpp:123
     Pose doubleSide = eye4();           // the optimised double-side transform (as a pose)
 
@@ -412,6 +443,9 @@ public:
     }
 protected:
     int model() const override { return MCC_MODEL_DOUBLESIDE; }
+    bool keepView(int) const override { return true; }   // storeReaded: every view (:114-118)
+    // findTimStamp (:100-112): another camera saw the OTHER side at the same timestamp
+    bool sameTimestampMatches(int n, int nOther) const override { return n != nOther; }
     void extraDesc(mcc_desc& d) override {
         _cp.clear();
         for (const Pose& P : camerasPose) _cp.insert(_cp.end(), P.begin(), P.end());

@@ -141,7 +141,9 @@ void MultiCameraCalibration::graphTraverse(int begin, std::vector<int>& order, s
     if (adjacency) *adjacency = std::move(adj);
 }
 
-void MultiCameraCalibration::initialize() {
+void MultiCameraCalibration::initialize() { chainPoses(true); }
+
+void MultiCameraCalibration::chainPoses(bool setCameras) {
     std::vector<int> order, pre;
     std::vector<std::vector<std::pair<int, int>>> adj;
     graphTraverse(0, order, pre, &adj);
@@ -173,8 +175,12 @@ void MultiCameraCalibration::initialize() {
             mul4(T, dsInv, t2);
             std::copy(t2, t2 + 16, T);
         }
-        if (v < _nCamera) mul4(T, preInv, out);    // camera: transform * prePose^-1
-        else mul4(preInv, T, out);                 // photo:  prePose^-1 * transform
+        if (v < _nCamera) {
+            if (!setCameras) continue;             // DoubleSide: fixed cameras
+            mul4(T, preInv, out);                  // camera: transform * prePose^-1
+        } else {
+            mul4(preInv, T, out);                  // photo:  prePose^-1 * transform
+        }
         _vertexList[v].pose = to_f(out);
         if (_verbose && v < _nCamera) std::cout << "initial pose for camera " << v << " set" << std::endl;
     }
@@ -256,7 +262,6 @@ MyMultiCameraCalibration::MyMultiCameraCalibration(const std::vector<std::string
 void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers) {
     namespace fsys = std::filesystem;
     if (!outliers.empty()) m_outliers = outliers;
-    const int frontN = _FrontPatternSize.width * _FrontPatternSize.height;
     const int backN = _BackPatternSize.width * _BackPatternSize.height;
     for (int cam = 0; cam < _nCamera; ++cam) {   // loadOneSerial (src/mymulticalib.cpp:262-301)
         const std::string folder = dataFolder + "/" + cameraSerials[cam];
@@ -292,7 +297,7 @@ void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers)
                 std::cout << "invalid pattern :" << invalidPoseCount << ", " << file << std::endl;
                 continue;
             }
-            if (n != frontN) continue;   // storeReaded: front-pattern views only (src/mymulticalib.cpp:237)
+            if (!keepView(n)) continue;   // storeReaded: MyMulti keeps front-pattern views only (:237)
             filesEachCameraFull[cam].push_back(file);
             timestampFull[cam].push_back(timestamp);
             timestampAvailable[cam].push_back(timestamp);
@@ -309,12 +314,16 @@ void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers)
     setOfTimestampIsMulticamera.clear();
     for (int cam = 0; cam < _nCamera; ++cam) {
         timestampIsMulticamera[cam].clear();
-        for (int ts : timestampAvailable[cam]) {
+        for (size_t i = 0; i < timestampAvailable[cam].size(); ++i) {
+            const int ts = timestampAvailable[cam][i];
+            const int n = (int)_imagePointsForEachCamera[cam][i].size() / 2;
             bool found = false;
-            for (int c2 = 0; c2 < _nCamera && !found; ++c2)
-                if (c2 != cam)
-                    found = std::find(timestampAvailable[c2].begin(), timestampAvailable[c2].end(), ts) !=
-                            timestampAvailable[c2].end();
+            for (int c2 = 0; c2 < _nCamera && !found; ++c2) {
+                if (c2 == cam) continue;
+                for (size_t j = 0; j < timestampAvailable[c2].size() && !found; ++j)
+                    found = timestampAvailable[c2][j] == ts &&
+                            sameTimestampMatches(n, (int)_imagePointsForEachCamera[c2][j].size() / 2);
+            }
             timestampIsMulticamera[cam].push_back(found);
             if (found) setOfTimestampIsMulticamera.insert(ts);
         }
@@ -386,6 +395,72 @@ void MyMultiCameraCalibration::writeParameters(const std::string& filename) {
             if (!mats[i].empty()) out.write(matNames[i], mats[i]);
         out.release();
     }
+}
+
+// ---------------------------------------------------------------- DoubleSideCalibration
+DoubleSideCalibration::DoubleSideCalibration(const std::vector<std::string>& serials, int cameraType, int nCameras,
+                                             const std::string& dataFolder_, const std::string& cameraConfigFolder_,
+                                             Size frontPatternSize, Size backPatternSize, float pw, float ph,
+                                             int verbose, int showExtration, int nMiniMatches, int flags,
+                                             TermCriteria criteria, int device)
+    : MyMultiCameraCalibration(serials, cameraType, nCameras, dataFolder_, cameraConfigFolder_, "", frontPatternSize,
+                               backPatternSize, pw, ph, verbose, showExtration, nMiniMatches, flags, criteria, device),
+      camerasPose(nCameras, eye4()) {
+    for (int c = 0; c < nCameras; ++c) {   // loadCameraPose (src/doubleSide.cpp:276-287)
+        const std::string fn = cameraConfigFolder + "/" + serials[c] + ".xml";
+        stg::FileStorage fs(fn, stg::FileStorage::READ);
+        const stg::Node& P = fs["CameraMatrix"];
+        if (P.type != stg::Node::MAT || P.mat.data.size() != 16) throw std::runtime_error(fn + ": CameraMatrix must be 4x4");
+        for (int k = 0; k < 16; ++k) camerasPose[c][k] = (float)P.mat.data[k];
+        _vertexList[c].pose = camerasPose[c];
+    }
+}
+
+void DoubleSideCalibration::initialize() {
+    // initializeDoublesideTransform: the first photo vertex with a FRONT and a BACK edge
+    int ef = -1, eb = -1;
+    for (size_t v = _nCamera; v < _vertexList.size() && (ef < 0 || eb < 0); ++v) {
+        ef = eb = -1;
+        for (size_t e = 0; e < _edgeList.size(); ++e) {
+            if (_edgeList[e].photoVertex != (int)v) continue;
+            if (_edgeList[e].patternSide == BACK_PATTERN) {
+                if (eb < 0) eb = (int)e;
+            } else if (ef < 0) {
+                ef = (int)e;
+            }
+        }
+    }
+    if (ef < 0 || eb < 0) throw std::runtime_error("DoubleSide initialize: no photo is seen from both sides");
+    // findTransformOfTwoEdge: frontpose = camPose_f^-1 T_f, backpose = camPose_b^-1 T_b,
+    // doubleSideTransform = frontpose^-1 backpose
+    double cf[16], cb[16], tf[16], tb[16], cfi[16], cbi[16], fp[16], bp[16], fpi[16], ds[16];
+    to_d(camerasPose[_edgeList[ef].cameraVertex], cf);
+    to_d(camerasPose[_edgeList[eb].cameraVertex], cb);
+    to_d(_edgeList[ef].transform, tf);
+    to_d(_edgeList[eb].transform, tb);
+    inv4(cf, cfi);
+    inv4(cb, cbi);
+    mul4(cfi, tf, fp);
+    mul4(cbi, tb, bp);
+    inv4(fp, fpi);
+    mul4(fpi, bp, ds);
+    for (int k = 0; k < 16; ++k) doubleSideTransform[k] = (double)(float)ds[k];   // CV_32F pose product
+    doubleSide = to_f(ds);
+    for (int c = 0; c < _nCamera; ++c) _vertexList[c].pose = camerasPose[c];
+    chainPoses(false);
+}
+
+void DoubleSideCalibration::writeParameters(const std::string&) {
+    stg::FileStorage fs("doublesideTransform.yaml", stg::FileStorage::WRITE);
+    stg::Mat T(4, 4, 'f');
+    for (int k = 0; k < 16; ++k) T.data[k] = doubleSide[k];
+    fs.write("transform", T);
+    fs.release();
+}
+
+void DoubleSideCalibration::reset() {
+    MyMultiCameraCalibration::reset();
+    for (int c = 0; c < _nCamera; ++c) _vertexList[c].pose = camerasPose[c];
 }
 
 }  // namespace multicalib

@@ -5,7 +5,12 @@
 //
 //   multi_cameras_calibration --serials S0,S1,... --data DIR --config DIR [--doubleside FILE]
 //       [--front 8x11] [--back 7x10] [--out multi-camera-results.xml] [--single-pass]
-//       [--init-only] [--dump-problem FILE] [--dump-result FILE] [--device N] [--verbose]
+//       [--double-side] [--init-only] [--dump-problem FILE] [--dump-result FILE] [--device N]
+//       [--verbose]
+//
+// --double-side runs DoubleSideCalibration instead (the reference sample's #else branch: fixed
+// camera poses from the configs' CameraMatrix, the double-side transform optimised; its
+// writeParameters writes doublesideTransform.yaml in the working directory).
 //
 // --init-only stops after loadImages + initialize (no GPU needed).  --dump-problem writes the
 // problem of the last pass (tests/cpp blob format + photo timestamps) with x0 = buildParas(),
@@ -14,6 +19,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <memory>
 #include <sstream>
 
 #include "mcc_multicalib.hpp"
@@ -61,10 +67,12 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
         img.insert(img.end(), im.begin(), im.end());
         corners += (int)o.size() / 3;
     }
+    auto* dsc = dynamic_cast<DoubleSideCalibration*>(&mc);
     bool has_ds = false;
-    for (double v : mc.doubleSideTransform) has_ds = has_ds || v != 0.0;
-    const int hdr[11] = {0x4d434331, MCC_MODEL_PINHOLE, C, V, E, nd, corners, has_ds ? 1 : 0, 0,
-                         mc._criteria.type, mc._criteria.maxCount};
+    if (!dsc)
+        for (double v : mc.doubleSideTransform) has_ds = has_ds || v != 0.0;
+    const int hdr[11] = {0x4d434331, dsc ? MCC_MODEL_DOUBLESIDE : MCC_MODEL_PINHOLE, C, V, E, nd, corners,
+                         has_ds ? 1 : 0, dsc ? 1 : 0, mc._criteria.type, mc._criteria.maxCount};
     std::ofstream f(path, std::ios::binary);
     wr(f, hdr, 11);
     wr(f, &mc._criteria.epsilon, 1);
@@ -75,6 +83,8 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
     for (int c = 0; c < C; ++c) wr(f, mc._distortCoeffs[c].data(), nd);
     wr(f, mc._xi.data(), C);
     if (has_ds) wr(f, mc.doubleSideTransform.data(), 16);
+    if (dsc)
+        for (int c = 0; c < C; ++c) wr(f, dsc->camerasPose[c].data(), 16);
     const std::vector<float> x0 = mc.buildParas();
     wr(f, x0.data(), x0.size());
     std::vector<int> ts;
@@ -88,7 +98,7 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
 int main(int argc, char** argv) {
     std::string serials, data, config, ds, out = "multi-camera-results.xml", dump_p, dump_r;
     Size front(8, 11), back(7, 10);
-    bool single = false, init_only = false;
+    bool single = false, init_only = false, double_side = false;
     int device = 0, verbose = 0;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -105,6 +115,7 @@ int main(int argc, char** argv) {
         else if (a == "--out") out = next();
         else if (a == "--single-pass") single = true;
         else if (a == "--init-only") init_only = true;
+        else if (a == "--double-side") double_side = true;
         else if (a == "--dump-problem") dump_p = next();
         else if (a == "--dump-result") dump_r = next();
         else if (a == "--device") device = std::stoi(next());
@@ -120,9 +131,18 @@ int main(int argc, char** argv) {
             std::fprintf(stderr, "usage: %s --serials S0,S1,... --data DIR --config DIR [options]\n", argv[0]);
             return 2;
         }
-        MyMultiCameraCalibration multiCalib(cams, MultiCameraCalibration::PINHOLE, (int)cams.size(), data, config, ds,
-                                            front, back, 0.f, 0.f, verbose, 0, 0, 0,
-                                            TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-7), device);
+        std::unique_ptr<MyMultiCameraCalibration> mc;
+        if (double_side)
+            mc.reset(new DoubleSideCalibration(cams, MultiCameraCalibration::PINHOLE, (int)cams.size(), data, config,
+                                               front, back, 0.f, 0.f, verbose, 0, 0, 0,
+                                               TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-8),
+                                               device));
+        else
+            mc.reset(new MyMultiCameraCalibration(cams, MultiCameraCalibration::PINHOLE, (int)cams.size(), data,
+                                                  config, ds, front, back, 0.f, 0.f, verbose, 0, 0, 0,
+                                                  TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 200, 1e-7),
+                                                  device));
+        MyMultiCameraCalibration& multiCalib = *mc;
         multiCalib.loadImages();
         multiCalib.initialize();
         if (init_only) {

@@ -49,7 +49,7 @@ def write_dataset(p: "rig.Problem", root: str, outlier_edges=(), outlier_px=2.0,
         with open(os.path.join(config, s + ".xml"), "w") as f:
             f.write('<?xml version="1.0"?>\n<opencv_storage>\n<depth_scale>1.0000000474974513e-03</depth_scale>\n'
                     "<height>480.</height>\n")
-            f.write(_mat_xml("CameraMatrix", np.eye(4)))
+            f.write(_mat_xml("CameraMatrix", p.cam_pose[c] if p.cam_pose is not None else np.eye(4)))
             f.write(_mat_xml("Intrinsics", p.K[c]))
             f.write(_mat_xml("Distortion", p.D[c][None, :]))
             f.write("</opencv_storage>\n")
@@ -68,7 +68,7 @@ def write_dataset(p: "rig.Problem", root: str, outlier_edges=(), outlier_px=2.0,
             f.write(_mat_yaml("corners", img))
             f.write(_mat_yaml("objects", np.asarray(p.obj[o:o + n], np.float64)))
         files[fn] = e
-    for c, s in enumerate(serials):   # back-pattern views (70 corners): dropped by storeReaded
+    for c, s in enumerate(serials):   # back-pattern views (70 corners): MyMulti's storeReaded drops them
         for k in range(back_views):
             e = int(np.nonzero(p.edge_cam == c)[0][k])
             o = int(p.edge_off[e])

@@ -174,3 +174,90 @@ def test_sample_two_pass_flow(sample, tmp_path):
         assert np.allclose(_xml_mat(croot, "CameraMatrix"), _xml_mat(root, f"camera_pose_{c}"))
         assert np.allclose(_xml_mat(croot, "Intrinsics"), p.K[c], rtol=1e-6)
         assert croot.find("depth_scale") is not None and croot.find("height") is not None
+
+
+# ---------------------------------------------------------------- DoubleSideCalibration
+def _ds_rig():
+    return rig.make_config("config5", n_views=16)
+
+
+def _expected_order_ds(p, stamps, skip_edges=()):
+    """DoubleSide loadImages: every view is stored; a view enters when another camera saw the
+    other side at the same timestamp (findTimStamp, src/doubleSide.cpp:100-112)."""
+    skip = set(int(e) for e in skip_edges)
+    edges = []
+    for c in range(p.n_cams):
+        es = [int(e) for e in np.nonzero(p.edge_cam == c)[0] if int(e) not in skip]
+        es.sort(key=lambda e: stamps[int(p.edge_photo[e])])
+        edges += es
+    sides = {}
+    for e in edges:
+        sides.setdefault(int(p.edge_photo[e]), set()).add(int(p.edge_n[e]))
+    edges = [e for e in edges if len(sides[int(p.edge_photo[e])]) >= 2]
+    photos = []
+    for e in edges:
+        if int(p.edge_photo[e]) not in photos:
+            photos.append(int(p.edge_photo[e]))
+    return edges, photos
+
+
+def _pose(x6):
+    P = np.eye(4)
+    P[:3, :3] = _rot(x6[:3])
+    P[:3, 3] = x6[3:]
+    return P
+
+
+def test_doubleside_load_initialize_cpu(sample, tmp_path):
+    p = _ds_rig()
+    serials, data, config, files, stamps = SD.write_dataset(p, str(tmp_path))
+    dump = str(tmp_path / "problem.bin")
+    _run(sample, ["--double-side", "--serials", ",".join(serials), "--data", data, "--config", config,
+                  "--init-only", "--dump-problem", dump])
+    q, ts = SD.read_dump(dump)
+    assert q.model == rig.DOUBLESIDE
+    edges, photos = _expected_order_ds(p, stamps)
+    assert q.n_edges == len(edges) and list(ts) == [int(stamps[ph]) for ph in photos]
+    assert np.array_equal(q.cam_pose, p.cam_pose)
+    for k, e in enumerate(edges):
+        assert int(q.edge_cam[k]) == int(p.edge_cam[e]) and int(q.edge_side[k]) == int(p.edge_side[e])
+        o, n, qo = int(p.edge_off[e]), int(p.edge_n[e]), int(q.edge_off[k])
+        assert np.array_equal(q.obj[qo:qo + n], p.obj[o:o + n]) and np.array_equal(q.img[qo:qo + n], p.img[o:o + n])
+    # the double-side transform from the first photo seen on both sides, then the photos
+    assert np.abs(_pose(q.x0[:6]) - _pose(p.x_true[:6]))[:3, :3].max() < 1e-2
+    assert np.abs(_pose(q.x0[:6]) - _pose(p.x_true[:6]))[:3, 3].max() < 20.0
+    for k, ph in enumerate(photos):
+        xq, xt = q.x0[6 + 6 * k:12 + 6 * k], p.x_true[p.photo_col(ph):p.photo_col(ph) + 6]
+        assert np.abs(_rot(xq[:3]) - _rot(xt[:3])).max() < 1e-2
+        assert np.abs(xq[3:] - xt[3:]).max() < 20.0
+
+
+@pytest.mark.gpu
+def test_doubleside_two_pass_flow(sample, tmp_path):
+    p = _ds_rig()
+    outl = [5, 30]
+    serials, data, config, files, stamps = SD.write_dataset(p, str(tmp_path), outlier_edges=outl)
+    dump, res = str(tmp_path / "problem.bin"), str(tmp_path / "result.txt")
+    r0 = subprocess.run([sample, "--double-side", "--serials", ",".join(serials), "--data", data, "--config", config,
+                         "--dump-problem", dump, "--dump-result", res], capture_output=True, text=True,
+                        timeout=300, cwd=str(tmp_path))
+    assert r0.returncode == 0, r0.stdout[-3000:] + r0.stderr[-3000:]
+    r = SD.read_result(res)
+    assert sorted(r["outliers"]) == sorted(fn for fn, e in files.items() if e in outl)
+    q, ts = SD.read_dump(dump)
+    edges, photos = _expected_order_ds(p, stamps, skip_edges=outl)
+    assert q.n_edges == len(edges)
+    x_ref, m_ref, it_ref, _ = O.Oracle(q).optimize(q.x0, 3, 200, 1e-8)   # DoubleSide's TermCriteria
+    assert r["iterations"] == it_ref
+    assert abs(r["error"] - m_ref) <= 1e-6
+    xo = r["x"].astype(np.float64).reshape(-1, 6)
+    xr = np.asarray(x_ref, np.float64).reshape(-1, 6)
+    for a, b in zip(xo, xr):
+        assert np.abs(_rot(a[:3]) - _rot(b[:3])).max() <= 1e-3
+    assert np.abs(xo[:, 3:] - xr[:, 3:]).max() <= 1e-4 * np.abs(xr[:, 3:]).max()
+    # writeParameters: doublesideTransform.yaml in the working directory, key "transform"
+    txt = open(tmp_path / "doublesideTransform.yaml").read()
+    vals = [float(v) for v in txt.split("data:")[1].replace("[", " ").replace("]", " ").replace(",", " ").split()]
+    T = np.array(vals).reshape(4, 4)
+    assert np.abs(T - _pose(xo[0])).max() <= 1e-3 * max(1.0, np.abs(T).max())
+    assert np.abs(T[:3, 3] - p.x_true[3:6]).max() < 5.0   # near the synthetic truth
