@@ -24,6 +24,7 @@ from . import rig as _rig
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MCC_LIB") or os.path.join(_HERE, "libmcc.so")   # MCC_LIB: libmcc_diag.so for stamps
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "mcc.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "mcc_omnidir.h")]   # the C ABI of libmcc.so
 
 _i32p = ctypes.POINTER(ctypes.c_int)
 _f32p = ctypes.POINTER(ctypes.c_float)
@@ -45,11 +46,17 @@ class _Desc(ctypes.Structure):
                 ("device", ctypes.c_int)]
 
 
+class _OmniDesc(ctypes.Structure):
+    _fields_ = [("n_views", ctypes.c_int), ("view_off", _i32p), ("obj", _f64p), ("img", _f64p),
+                ("flags", ctypes.c_int), ("device", ctypes.c_int)]
+
+
 _LIB = None
 
 
 HOST_LIB_PATH = os.path.join(_HERE, "libmcc_host.so")
 SAMPLE_PATH = os.path.join(_HERE, "build", "multi_cameras_calibration")
+OMNI_SAMPLE_PATH = os.path.join(_HERE, "build", "omni_calibration")
 
 
 def build(force: bool = False) -> str:
@@ -58,7 +65,7 @@ def build(force: bool = False) -> str:
     inc = os.path.dirname(HEADER)
     srcs = [os.path.join(_HERE, d, f) for d in ("csrc", "host", "samples") for f in os.listdir(os.path.join(_HERE, d))]
     srcs += [os.path.join(inc, f) for f in os.listdir(inc)]
-    outs = [LIB_PATH, HOST_LIB_PATH, SAMPLE_PATH]
+    outs = [LIB_PATH, HOST_LIB_PATH, SAMPLE_PATH, OMNI_SAMPLE_PATH]
     stale = any(not os.path.exists(o) for o in outs) or any(
         os.path.getmtime(s) > min(os.path.getmtime(o) for o in outs) for s in srcs)
     if force or stale:
@@ -99,13 +106,28 @@ def lib():
         L.mcc_peer_handle.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.mcc_peer_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.mcc_peer_enable.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        # include/mcc_omnidir.h
+        L.mcc_omnicalib_create.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_OmniDesc)]
+        L.mcc_omnicalib_destroy.argtypes = [ctypes.c_void_p]
+        L.mcc_omnicalib_destroy.restype = None
+        L.mcc_omnicalib_nparams.argtypes = [ctypes.c_void_p]
+        L.mcc_omnicalib_jacobian.argtypes = [ctypes.c_void_p, _f64p, ctypes.c_int, _f64p, _f64p]
+        L.mcc_omnicalib_optimize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_double, _f64p,
+                                             _i32p, _f64p]
+        L.mcc_omnicalib_rms.argtypes = [ctypes.c_void_p, _f64p, _f64p]
+        L.mcc_omnicalib_time_steps.argtypes = [ctypes.c_void_p, _f64p, ctypes.c_int, _f64p]
+        L.mcc_omnidir_initialize.argtypes = [ctypes.c_int, _i32p, _f64p, _f64p, ctypes.c_int, ctypes.c_int, _f64p,
+                                             _f64p, _f64p, _f64p, _i32p, _i32p]
+        L.mcc_omnidir_calibrate.argtypes = [ctypes.c_int, _i32p, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                            _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _i32p, _f64p, _i32p]
         _LIB = L
     return _LIB
 
 
 def declared_symbols():
-    """Every function include/mcc.h declares."""
-    txt = open(HEADER).read()
+    """Every function the C-ABI headers of libmcc.so (include/mcc.h, include/mcc_omnidir.h) declare."""
+    txt = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(mcc_[a-z_]+)\s*\(", txt, re.M)))
 
 
@@ -300,3 +322,110 @@ class BundleAdjuster:
 
     def peer_enable(self, on: bool):
         _check(lib().mcc_peer_enable(self.h, int(bool(on))), "mcc_peer_enable")
+
+
+# ---------------------------------------------------------------- cv::omnidir::calibrate
+# include/mcc_omnidir.h; the reference's names: cv::omnidir::calibrate (src/omnidir.cpp:1067-1211),
+# internal::initializeCalibration (:551-748), internal::computeJacobian (:851-935).
+CALIB_USE_GUESS, CALIB_FIX_SKEW, CALIB_FIX_K1, CALIB_FIX_K2 = 1, 2, 4, 8
+CALIB_FIX_P1, CALIB_FIX_P2, CALIB_FIX_XI, CALIB_FIX_GAMMA, CALIB_FIX_CENTER = 16, 32, 64, 128, 256
+
+
+def _views(off, obj, img):
+    off = np.ascontiguousarray(off, np.int32)
+    obj = np.ascontiguousarray(obj, np.float64).reshape(-1, 3)
+    img = np.ascontiguousarray(img, np.float64).reshape(-1, 2)
+    if off.ndim != 1 or off.size < 2 or off[0] != 0 or off[-1] != obj.shape[0] or obj.shape[0] != img.shape[0]:
+        raise MccError("view offsets / points mismatch")
+    return off, obj, img
+
+
+class OmniCalibrator:
+    """The device-resident state of cv::omnidir::calibrate's loop for one camera's views
+    (CV_64F pattern / image points, parameters in encodeParameters layout, P = 6n + 10)."""
+
+    def __init__(self, off, obj, img, flags: int = 0, device: int = 0):
+        self.off, self.obj, self.img = _views(off, obj, img)
+        d = _OmniDesc()
+        d.n_views = self.off.size - 1
+        d.view_off = _ptr(self.off, _i32p)
+        d.obj = _ptr(self.obj, _f64p)
+        d.img = _ptr(self.img, _f64p)
+        d.flags, d.device = flags, device
+        h = ctypes.c_void_p()
+        _check(lib().mcc_omnicalib_create(ctypes.byref(h), ctypes.byref(d)), "mcc_omnicalib_create")
+        self.h = h
+        self.P = lib().mcc_omnicalib_nparams(h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mcc_omnicalib_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compute_jacobian(self, params, it=0):
+        """(JTE before the flag reduction, G of loop iteration `it`) at params (computeJacobian)."""
+        p = np.ascontiguousarray(params, np.float64)
+        jte, G = np.zeros(self.P), np.zeros(self.P)
+        _check(lib().mcc_omnicalib_jacobian(self.h, _ptr(p, _f64p), it, _ptr(jte, _f64p), _ptr(G, _f64p)),
+               "mcc_omnicalib_jacobian")
+        return jte, G
+
+    def optimize(self, params, crit_type=MCC_CRIT_COUNT_EPS, max_count=200, eps=1e-4):
+        """calibrate's loop: (params, iterations, last change)."""
+        p = np.array(params, np.float64, copy=True)
+        it, ch = ctypes.c_int(0), ctypes.c_double(0)
+        _check(lib().mcc_omnicalib_optimize(self.h, crit_type, max_count, eps, _ptr(p, _f64p), ctypes.byref(it),
+                                            ctypes.byref(ch)), "mcc_omnicalib_optimize")
+        return p, it.value, ch.value
+
+    def rms(self, params):
+        p = np.ascontiguousarray(params, np.float64)
+        r = ctypes.c_double(0)
+        _check(lib().mcc_omnicalib_rms(self.h, _ptr(p, _f64p), ctypes.byref(r)), "mcc_omnicalib_rms")
+        return r.value
+
+    def time_steps(self, params, n_steps):
+        p = np.ascontiguousarray(params, np.float64)
+        ms = ctypes.c_double(0)
+        _check(lib().mcc_omnicalib_time_steps(self.h, _ptr(p, _f64p), n_steps, ctypes.byref(ms)),
+               "mcc_omnicalib_time_steps")
+        return ms.value
+
+
+def omnidir_initialize(off, obj, img, image_size):
+    """initializeCalibration: (om[k, 3], t[k, 3], K 3x3, xi, idx[k]) -- host code, no GPU."""
+    off, obj, img = _views(off, obj, img)
+    n = off.size - 1
+    om, t, K = np.zeros((n, 3)), np.zeros((n, 3)), np.zeros(9)
+    xi, nk = ctypes.c_double(0), ctypes.c_int(0)
+    idx = np.zeros(n, np.int32)
+    _check(lib().mcc_omnidir_initialize(n, _ptr(off, _i32p), _ptr(obj, _f64p), _ptr(img, _f64p), int(image_size[0]),
+                                        int(image_size[1]), _ptr(om, _f64p), _ptr(t, _f64p), _ptr(K, _f64p),
+                                        ctypes.byref(xi), _ptr(idx, _i32p), ctypes.byref(nk)),
+           "mcc_omnidir_initialize")
+    k = nk.value
+    return om[:k], t[:k], K.reshape(3, 3), xi.value, idx[:k].copy()
+
+
+def omnidir_calibrate(off, obj, img, image_size, flags=0, crit_type=MCC_CRIT_COUNT_EPS, max_count=200, eps=1e-4,
+                      device=0):
+    """cv::omnidir::calibrate: (rms, K, xi, D, om[k, 3], t[k, 3], idx[k], iterations)."""
+    off, obj, img = _views(off, obj, img)
+    n = off.size - 1
+    K, D = np.zeros(9), np.zeros(4)
+    om, t = np.zeros((n, 3)), np.zeros((n, 3))
+    xi, rms, nk, it = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int(0), ctypes.c_int(0)
+    idx = np.zeros(n, np.int32)
+    _check(lib().mcc_omnidir_calibrate(n, _ptr(off, _i32p), _ptr(obj, _f64p), _ptr(img, _f64p), int(image_size[0]),
+                                       int(image_size[1]), flags, crit_type, max_count, eps, device, _ptr(K, _f64p),
+                                       ctypes.byref(xi), _ptr(D, _f64p), _ptr(om, _f64p), _ptr(t, _f64p),
+                                       _ptr(idx, _i32p), ctypes.byref(nk), ctypes.byref(rms), ctypes.byref(it)),
+           "mcc_omnidir_calibrate")
+    k = nk.value
+    return rms.value, K.reshape(3, 3), xi.value, D, om[:k], t[:k], idx[:k].copy(), it.value

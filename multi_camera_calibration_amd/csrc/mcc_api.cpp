@@ -357,6 +357,12 @@ extern "C" {
 
 const char* mcc_last_error(void) { return g_err.c_str(); }
 
+// the other C-ABI translation units (mcc_omnicalib_api.cpp) report through the same message slot
+__attribute__((visibility("hidden"))) int mcc_internal_fail(int code, const char* msg) { return fail(code, msg); }
+__attribute__((visibility("hidden"))) void mcc_internal_rodrigues_m2v(const double* R, double* r) {
+    host_rodrigues_m2v(R, r);
+}
+
 int mcc_nparams(const mcc_problem* p) { return p ? p->P : 0; }
 int mcc_global_dim(const mcc_problem* p) { return p ? p->m : 0; }
 

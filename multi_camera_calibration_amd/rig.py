@@ -464,3 +464,69 @@ def problem_from_arrays(a, prefix: str = "", name: str = "") -> Problem:
     kw = {f: (np.array(a[prefix + f]) if (prefix + f) in a else None) for f in _ARRAY_FIELDS}
     return Problem(model=meta[0], n_cams=meta[1], n_photos=meta[2], image_size=(meta[3], meta[4]),
                    name=name, **kw)
+
+
+# ----------------------------------------------------------------------------- omni intrinsic views
+@dataclasses.dataclass
+class OmniCalibViews:
+    """One omnidirectional camera's per-view chessboard corners, as cv::omnidir::calibrate takes
+    them (src/omnidir.cpp:1067-1090; CV_64F after its convertTo): view i holds corners
+    off[i]..off[i+1] of obj (x, y, 0) and img (u, v)."""
+    off: np.ndarray           # int32 [n+1]
+    obj: np.ndarray           # float64 [corners, 3]
+    img: np.ndarray           # float64 [corners, 2]
+    image_size: tuple         # (width, height)
+    K: np.ndarray             # truth (information only)
+    xi: float
+    D: np.ndarray
+    om: np.ndarray            # [n, 3]
+    t: np.ndarray             # [n, 3]
+
+    @property
+    def n_views(self) -> int:
+        return len(self.off) - 1
+
+
+def make_omni_views(n_views=1000, board=(11, 8), square=40.0, seed=4, noise_px=0.2,
+                    size=(1280, 960)) -> OmniCalibViews:
+    """Mei-model camera (config 4's intrinsics: f ~ 350, xi ~ U(0.8, 1.2), 1280x960, D = 4) and
+    n_views board poses 350-1300 mm away, up to 55 deg off axis, tilted up to 45 deg, every corner
+    inside the image with a 20 px margin; 0.2 px Gaussian corner noise."""
+    rng = np.random.default_rng(seed)
+    W, H = size
+    f = 350.0 * rng.uniform(0.97, 1.03)
+    K = np.array([[f, 0.0, W / 2 + rng.uniform(-10, 10)], [0, f * rng.uniform(0.99, 1.01), H / 2 + rng.uniform(-10, 10)],
+                  [0, 0, 1]])
+    xi = float(rng.uniform(0.8, 1.2))
+    D = np.array([rng.uniform(-0.1, 0.0), rng.uniform(0.0, 0.05), rng.uniform(-5e-4, 5e-4), rng.uniform(-5e-4, 5e-4)])
+    pts = board_points(board[0], board[1], square)
+    ctr = pts.mean(0)
+    oms, ts, imgs = [], [], []
+    margin = 20.0
+    while len(oms) < n_views:
+        dist = rng.uniform(350.0, 1300.0)
+        off_ang = np.deg2rad(rng.uniform(0, 55))
+        az = rng.uniform(-np.pi, np.pi)
+        dirv = np.array([np.sin(off_ang) * np.cos(az), np.sin(off_ang) * np.sin(az), np.cos(off_ang)])
+        center = dist * dirv
+        # board normal roughly facing the camera, tilted up to 45 deg, random in-plane spin
+        R0 = look_at(np.zeros(3), center)   # camera looking at the board centre
+        tilt = rng.normal(size=3)
+        tilt *= np.deg2rad(rng.uniform(0, 45)) / np.linalg.norm(tilt)
+        spin = rodrigues(np.array([0.0, 0.0, rng.uniform(-np.pi, np.pi)]))
+        Rb = R0.T @ rodrigues(tilt) @ spin            # board -> camera rotation
+        tb = center - Rb @ ctr
+        Xc = pts @ Rb.T + tb
+        if np.any(Xc[:, 2] < 50.0):
+            continue
+        uv = project_omni(Xc, K, xi, D)
+        if np.any(uv[:, 0] < margin) or np.any(uv[:, 0] > W - margin) or np.any(uv[:, 1] < margin) \
+                or np.any(uv[:, 1] > H - margin):
+            continue
+        oms.append(log_so3(Rb))
+        ts.append(tb)
+        imgs.append(uv + rng.normal(scale=noise_px, size=uv.shape))
+    n = len(oms)
+    off = np.arange(n + 1, dtype=np.int32) * len(pts)
+    return OmniCalibViews(off, np.tile(pts, (n, 1)), np.concatenate(imgs), (W, H), K, xi, D,
+                          np.array(oms), np.array(ts))

@@ -122,6 +122,28 @@ double ora_optimize(const ora_problem *p, int crit_type, int max_count, double e
  * ((double)float-total / totalNPoints, with totalNPoints = 2N pinhole / N omni). */
 int ora_project_error(const ora_problem *p, const float *x, float *edge_err, double *mean);
 
+/* ---- cv::omnidir::calibrate, mcc_oracle_omnicalib.c.  Parameters in the
+ * reference's encodeParameters layout: [om_i(3), T_i(3)] x n, fx, fy, s, cx, cy, xi, k1, k2, p1, p2
+ * (P = 6n + 10), CV_64F.  Views are [off[i], off[i+1]) ranges of obj (xyz) / img (uv). */
+/* projectPoints with the 2x16 Jacobian (JacobianRow order); kin = fx, fy, s, cx, cy */
+void ora_omni_project_full(int n, const double *obj, const double om[3], const double T[3],
+                           const double kin[5], double xi, const double D[4], double *img, double *jac);
+void ora_omni_flags2idx(int flags, int n, int *idx);
+/* computeJacobian: JTE before subMatrix (P), and/or (JTJ + epsilon)^-1 and JTE after it (n_free) */
+int ora_omni_jacobian(int n, const int *off, const double *obj, const double *img, const double *para,
+                      int flags, double epsilon, double *JTJ_inv, double *JTE_full, double *JTE_sub, int *n_free);
+/* G of the loop at iteration iter (alpha_smooth2, epsilon, fillFixed), P long */
+int ora_omni_step(int n, const int *off, const double *obj, const double *img, const double *para,
+                  int flags, int iter, double *G);
+int ora_omni_optimize(int n, const int *off, const double *obj, const double *img, double *para, int flags,
+                      int crit_type, int max_count, double eps, int *iters, double *last_change);
+double ora_omni_rms(int n, const int *off, const double *obj, const double *img, const double *para);
+int ora_omni_init(int n_img, const int *off, const double *obj, const double *img, int width, int height,
+                  double *om_out, double *t_out, double *K, double *xi, int *idx, int *n_idx);
+double ora_omni_calibrate(int n_img, const int *off, const double *obj, const double *img, int width, int height,
+                          int flags, int crit_type, int max_count, double eps, double *K, double *xi, double *D,
+                          double *om, double *t, int *idx, int *n_idx, int *iters);
+
 /* OpenMP threads the oracle uses (1 if built without OpenMP). */
 int ora_num_threads(void);
 

@@ -29,8 +29,8 @@ class _OraProblem(ctypes.Structure):
 
 def build(force: bool = False) -> str:
     so = os.path.join(_HERE, "liboracle.so")
-    src = os.path.join(_HERE, "mcc_oracle.c")
-    if force or not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("mcc_oracle.c", "mcc_oracle_omnicalib.c", "mcc_oracle.h")]
+    if force or not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(f) for f in srcs):
         subprocess.run(["make", "-C", _HERE, "-s", "liboracle.so"], check=True)
     return so
 
@@ -42,6 +42,8 @@ def lib():
         L = _LIB
         L.ora_optimize.restype = ctypes.c_double
         L.ora_num_threads.restype = ctypes.c_int
+        L.ora_omni_rms.restype = ctypes.c_double
+        L.ora_omni_calibrate.restype = ctypes.c_double
     return _LIB
 
 
@@ -196,3 +198,118 @@ def project_omni(obj, rvec, tvec, K, xi, D, jac=True):
 
 def num_threads():
     return lib().ora_num_threads()
+
+
+# ---------------------------------------------------------------- cv::omnidir::calibrate
+class OmniViews:
+    """Per-view corner sets of one camera, as cv::omnidir::calibrate takes them (CV_64F):
+    off[n+1] corner ranges, obj (corners x 3), img (corners x 2)."""
+
+    def __init__(self, off, obj, img):
+        self.off = np.ascontiguousarray(off, np.int32)
+        self.obj = np.ascontiguousarray(obj, np.float64).reshape(-1, 3)
+        self.img = np.ascontiguousarray(img, np.float64).reshape(-1, 2)
+        self.n = len(self.off) - 1
+
+    @property
+    def n_params(self):
+        return 6 * self.n + 10
+
+    def args(self):
+        return (self.n, _p(self.off, _i32p), _p(self.obj, _f64p), _p(self.img, _f64p))
+
+    def subset(self, idx):
+        idx = list(idx)
+        offs = [0]
+        for i in idx:
+            offs.append(offs[-1] + int(self.off[i + 1] - self.off[i]))
+        sel = np.concatenate([np.arange(self.off[i], self.off[i + 1]) for i in idx]) if idx else np.zeros(0, int)
+        return OmniViews(np.array(offs, np.int32), self.obj[sel], self.img[sel])
+
+
+def omni_project_full(obj, om, T, kin, xi, D, jac=True):
+    obj = np.ascontiguousarray(obj, np.float64).reshape(-1, 3)
+    n = obj.shape[0]
+    a = [np.ascontiguousarray(v, np.float64) for v in (om, T, kin, D)]
+    img = np.zeros(2 * n)
+    J = np.zeros((2 * n, 16)) if jac else None
+    lib().ora_omni_project_full(n, _p(obj, _f64p), _p(a[0], _f64p), _p(a[1], _f64p), _p(a[2], _f64p),
+                                ctypes.c_double(xi), _p(a[3], _f64p), _p(img, _f64p), _p(J, _f64p))
+    return img.reshape(n, 2), J
+
+
+def omni_flags2idx(flags, n):
+    idx = np.zeros(6 * n + 10, np.int32)
+    lib().ora_omni_flags2idx(flags, n, _p(idx, _i32p))
+    return idx
+
+
+def omni_jacobian(v: OmniViews, para, flags=0, epsilon=0.0, inverse=True):
+    """computeJacobian: (JTE before subMatrix, (JTJ + eps)^-1 after it, JTE after it)"""
+    para = np.ascontiguousarray(para, np.float64)
+    P = v.n_params
+    nf = ctypes.c_int(0)
+    full = np.zeros(P)
+    Ji = np.zeros((P, P)) if inverse else None
+    sub = np.zeros(P)
+    rc = lib().ora_omni_jacobian(*v.args(), _p(para, _f64p), flags, ctypes.c_double(epsilon), _p(Ji, _f64p),
+                                 _p(full, _f64p), _p(sub, _f64p), ctypes.byref(nf))
+    if rc:
+        raise RuntimeError(f"ora_omni_jacobian failed: {rc}")
+    k = nf.value
+    return full, (Ji.reshape(-1)[:k * k].reshape(k, k) if inverse else None), sub[:k]
+
+
+def omni_step(v: OmniViews, para, flags, it):
+    para = np.ascontiguousarray(para, np.float64)
+    G = np.zeros(v.n_params)
+    rc = lib().ora_omni_step(*v.args(), _p(para, _f64p), flags, it, _p(G, _f64p))
+    if rc:
+        raise RuntimeError(f"ora_omni_step failed: {rc}")
+    return G
+
+
+def omni_optimize(v: OmniViews, para, flags=0, crit_type=3, max_count=200, eps=1e-4):
+    para = np.array(para, np.float64, copy=True)
+    it = ctypes.c_int(0); ch = ctypes.c_double(0)
+    rc = lib().ora_omni_optimize(*v.args(), _p(para, _f64p), flags, crit_type, max_count, ctypes.c_double(eps),
+                                 ctypes.byref(it), ctypes.byref(ch))
+    if rc:
+        raise RuntimeError(f"ora_omni_optimize failed: {rc}")
+    return para, it.value, ch.value
+
+
+def omni_rms(v: OmniViews, para):
+    para = np.ascontiguousarray(para, np.float64)
+    return lib().ora_omni_rms(*v.args(), _p(para, _f64p))
+
+
+def omni_init(v: OmniViews, width, height):
+    """initializeCalibration: (om[k,3], t[k,3], K 3x3, xi, idx[k])"""
+    om = np.zeros((v.n, 3)); t = np.zeros((v.n, 3)); K = np.zeros(9); xi = ctypes.c_double(0)
+    idx = np.zeros(max(v.n, 1), np.int32); nk = ctypes.c_int(0)
+    lib().ora_omni_init(*v.args(), width, height, _p(om, _f64p), _p(t, _f64p), _p(K, _f64p), ctypes.byref(xi),
+                        _p(idx, _i32p), ctypes.byref(nk))
+    k = nk.value
+    return om[:k], t[:k], K.reshape(3, 3), xi.value, idx[:k].copy()
+
+
+def omni_encode(om, t, K, xi, D=(0, 0, 0, 0)):
+    """encodeParameters, src/omnidir.cpp:1541-1568"""
+    K = np.asarray(K, np.float64).reshape(3, 3)
+    return np.concatenate([np.concatenate([om, t], axis=1).reshape(-1),
+                           [K[0, 0], K[1, 1], K[0, 1], K[0, 2], K[1, 2], xi], np.asarray(D, np.float64)])
+
+
+def omni_calibrate(v: OmniViews, width, height, flags=0, crit_type=3, max_count=200, eps=1e-4):
+    """cv::omnidir::calibrate: (rms, K, xi, D, om, t, idx, iters)"""
+    K = np.zeros(9); xi = ctypes.c_double(0); D = np.zeros(4)
+    om = np.zeros((v.n, 3)); t = np.zeros((v.n, 3)); idx = np.zeros(max(v.n, 1), np.int32)
+    nk = ctypes.c_int(0); it = ctypes.c_int(0)
+    rms = lib().ora_omni_calibrate(*v.args(), width, height, flags, crit_type, max_count, ctypes.c_double(eps),
+                                   _p(K, _f64p), ctypes.byref(xi), _p(D, _f64p), _p(om, _f64p), _p(t, _f64p),
+                                   _p(idx, _i32p), ctypes.byref(nk), ctypes.byref(it))
+    if rms < 0:
+        raise RuntimeError("ora_omni_calibrate failed")
+    k = nk.value
+    return rms, K.reshape(3, 3), xi.value, D, om[:k], t[:k], idx[:k].copy(), it.value
