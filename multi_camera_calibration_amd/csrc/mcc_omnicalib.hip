@@ -61,6 +61,21 @@ __device__ __forceinline__ double oc_readlane(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// sum_{q < n} p[q * kOcLc] in q order; the sc1 loads are issued 16 at a time so a group costs one
+// or two memory round trips instead of n dependent ones
+__device__ __forceinline__ double oc_sum(const double* p, int n) {
+    constexpr int B = 16;
+    double v = 0.0;
+    for (int q0 = 0; q0 < n; q0 += B) {
+        double b[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) b[u] = oc_ld(p + (size_t)min(q0 + u, n - 1) * kOcLc);
+#pragma unroll
+        for (int u = 0; u < B; ++u) v += q0 + u < n ? b[u] : 0.0;
+    }
+    return v;
+}
+
 // packed upper-triangle index of (i, j), i <= j, of a 10 x 10 matrix (row i holds 10 - i entries)
 __device__ __forceinline__ int oc_up(int i, int j) { return i * 10 - (i * (i - 1)) / 2 + (j - i); }
 
@@ -328,17 +343,9 @@ __global__ __launch_bounds__(256) void k_oc_step(OcArgs a) {
     // ---- two-level fixed-order reduction of the contributions
     const int grp = v / a.group_size, g0 = grp * a.group_size, gn = min(a.group_size, n - g0);
     if (!oc_arrive(&a.cnt[grp], gn)) return;
-    if (tid < kOcLc) {
-        double s = 0.0;
-        for (int q = 0; q < gn; ++q) s += oc_ld(a.contrib + (size_t)(g0 + q) * kOcLc + tid);
-        oc_st(a.gsum + (size_t)grp * kOcLc + tid, s);
-    }
+    if (tid < kOcLc) oc_st(a.gsum + (size_t)grp * kOcLc + tid, oc_sum(a.contrib + (size_t)g0 * kOcLc + tid, gn));
     if (!oc_arrive(&a.cnt[a.n_groups], a.n_groups)) return;
-    if (tid < kOcLc) {
-        double s = 0.0;
-        for (int q = 0; q < a.n_groups; ++q) s += oc_ld(a.gsum + (size_t)q * kOcLc + tid);
-        tot[tid] = s;
-    }
+    if (tid < kOcLc) tot[tid] = oc_sum(a.gsum + tid, a.n_groups);
     __syncthreads();
     if (wave != 0) return;
 
@@ -366,24 +373,51 @@ __global__ __launch_bounds__(256) void k_oc_step(OcArgs a) {
     }
     row[10] = free_i ? tot[kOcRb + li] : 0.0;
     row[11] = free_i ? 1.0 - tot[kOcWu + li] : 0.0;
+    // Gauss-Jordan, lane l keeps row l.  S is symmetric but can turn numerically indefinite (the
+    // f / xi coupling of the Mei model makes it near-singular, as is the reference's dense JTJ): a
+    // non-positive diagonal pivot falls back to the unused row of largest |entry|; an exactly singular
+    // system gives G = 0 for the whole step, as the reference's Mat::inv() (DECOMP_LU) returns a
+    // zero matrix then
+    bool used = lane >= 10, singular = false;
+    int pcol = -1;
     double dii = 1.0;
-    bool bad = false;
 #pragma unroll
     for (int kk = 0; kk < 10; ++kk) {
-        const double piv = oc_readlane(row[kk], kk);
-        bad |= !(piv > 0.0);
-        const double pv = piv > 0.0 ? piv : 1.0;
-        const double ip = 1.0 / pv;
-        if (lane == kk) dii = pv;
-        const double f = lane == kk ? 0.0 : row[kk] * ip;
+        // the diagonal in natural order while it is positive: the elimination order of the
+        // reference's dense LU on this (near-SPD) block, whose rounding the step reproduces
+        int pl = kk;
+        if (!(oc_readlane(row[kk], kk) > 0.0) || __builtin_amdgcn_readlane((int)used, kk) != 0) {
+            pl = -1;
+            double best = 0.0;
+#pragma unroll
+            for (int l = 0; l < 10; ++l) {
+                const double c = fabs(oc_readlane(row[kk], l));
+                const bool u = __builtin_amdgcn_readlane((int)used, l) != 0;
+                if (!u && c > best) { best = c; pl = l; }
+            }
+            if (pl < 0) { singular = true; break; }
+        }
+        const double piv = oc_readlane(row[kk], pl);
+        const double ip = 1.0 / piv;
+        if (lane == pl) { dii = piv; used = true; pcol = kk; }
+        const double f = lane == pl ? 0.0 : row[kk] * ip;
         double pr[12];
 #pragma unroll
-        for (int j = kk + 1; j < 12; ++j) pr[j] = oc_readlane(row[j], kk);
+        for (int j = kk + 1; j < 12; ++j) pr[j] = oc_readlane(row[j], pl);
 #pragma unroll
         for (int j = kk + 1; j < 12; ++j) row[j] -= f * pr[j];
     }
-    const double yb = lane < 10 ? row[10] / dii : 0.0;
-    const double yu = lane < 10 ? row[11] / dii : 0.0;
+    // lane j takes the solution of column j from the lane that pivoted it
+    const double sb = lane < 10 && !singular ? row[10] / dii : 0.0;
+    const double su = lane < 10 && !singular ? row[11] / dii : 0.0;
+    double yb = 0.0, yu = 0.0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const unsigned long long own = __ballot(pcol == j);
+        const int src = own ? (int)__builtin_ctzll(own) : 0;
+        const double vb = oc_readlane(sb, src), vu = oc_readlane(su, src);
+        if (lane == j) { yb = vb; yu = vu; }
+    }
     // 1^T A^-1 b = sum_v 1^T U^-1 rp_v - (sum_v W_v^T U^-1 1)^T yb + 1_free^T yb (and for u)
     const double wm = lane < 10 ? msk[lane] - tot[kOcWu + lane] : 0.0;
     double s1 = tot[kOcAb], s2 = tot[kOcAu];
@@ -392,9 +426,13 @@ __global__ __launch_bounds__(256) void k_oc_step(OcArgs a) {
         s1 += oc_readlane(wm * yb, l);
         s2 += oc_readlane(wm * yu, l);
     }
-    const double coef = epsilon * s1 / (1.0 + epsilon * s2);
-    const double yc = yb - coef * yu;
-    const double gc = alpha2 * yc;
+    double coef = epsilon * s1 / (1.0 + epsilon * s2);
+    // A + epsilon 1 1^T singular (Sherman-Morrison denominator 0) or A singular: G = 0 for the step
+    const bool skip = singular || !isfinite(coef);
+    if (skip) coef = 0.0;
+    const double yc = skip ? 0.0 : yb - coef * yu;
+    const double a2 = skip ? 0.0 : alpha2;
+    const double gc = a2 * yc;
     double ng = 0.0, nx = 0.0;
     double xo = 0.0;
     if (lane < 10) {
@@ -412,11 +450,10 @@ __global__ __launch_bounds__(256) void k_oc_step(OcArgs a) {
     if (lane == 0) {
         st->normG2_c = ng;
         st->normX2_c = nx;
-        st->alpha2 = alpha2;
+        st->alpha2 = a2;   // 0: the poses' pending G is 0 too
         st->coef = coef;
         st->pending = 1;
         st->iter = k + 1;
-        if (bad) st->error |= 2;
     }
 }
 
