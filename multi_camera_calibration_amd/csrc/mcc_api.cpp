@@ -124,7 +124,7 @@ struct mcc_problem {
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
-    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt;
+    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
@@ -239,6 +239,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.n_items = p->n_items;
     sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
     sa.counter = p->counter.p;
+    sa.cnt_blk = p->cnt_blk.p;
+    sa.nblk = p->nblk;
     sa.block_items = p->block_items.p;
     sa.packed = p->packed.p;
     // m > 30: the register-tiled elimination runs in its own kernel (k_solve)
@@ -483,6 +485,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         // (4 per sub-chunk thread) keeps the item workgroups busy
         const int per_item = std::max(20, (end - begin + 23) / 24);
         for (int s = begin; s < end; s += per_item) items.push_back(make_int4(b, s, std::min(end, s + per_item), 0));
+        // a block no photo couples gets one empty item: its last arriver writes the block's zeros
+        // (every packed entry is rewritten each step; the all-reduce leaves sums there)
+        if (begin == end) items.push_back(make_int4(b, begin, end, 0));
         block_items[b + 1] = (int)items.size();
     }
     for (int b1 = 0; b1 < nb; ++b1)
@@ -553,6 +558,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(hipMemset(p->item_out.p, 0, sizeof(double) * p->item_out.n));
     HIPC(p->counter.alloc(1));
     HIPC(hipMemset(p->counter.p, 0, sizeof(int)));
+    HIPC(p->cnt_blk.alloc(p->nblk));
+    HIPC(hipMemset(p->cnt_blk.p, 0, sizeof(int) * std::max(p->nblk, 1)));
     p->ntri = p->m * (p->m + 1) / 2;
     p->packed_len = p->ntri + 2 * p->m + 2;
     HIPC(p->packed.alloc(p->packed_len));
@@ -603,7 +610,7 @@ void mcc_destroy(mcc_problem* p) {
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Hgp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
-    p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release();
+    p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);

@@ -96,7 +96,9 @@ struct SchurArgs {
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;
     const double* photo_norm; int n_photos;
-    int* counter;        // ticket for the last-arriving workgroup (zero between launches)
+    int* counter;        // level-2 ticket over blocks + norm chunks (zero between launches)
+    int* cnt_blk;        // [nblk] level-1 tickets: the last item of a camera-pair block sums it
+    int nblk;
     const int* block_items;   // [nblk + 1]
     double* packed;
     int m, rank, fuse_solve;

@@ -1645,9 +1645,11 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 // ---------------------------------------------------------------- k_schur
 // Work item: pairs [begin, end) of one camera-pair block (S_ab -= Y'_a Hgp_b^T, r_a += gg_a - Y'_a gp).  Thread t < 240: entry q = t % 48
 // (0..35: S entry, 36..41: r entry, 42..47: JTE of the global block), sub-chunk s = t / 48.
-// Norm items sum 256 photos' norm partials.  The last workgroup to finish assembles the packed
-// system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2] in fixed order, and with
-// fuse_solve (single GPU) solves it in place.
+// Norm items sum 256 photos' norm partials.  Hand-off in two write-through levels (sc1 stores,
+// tickets, no fences): the last item of each camera-pair block sums the block's items in item
+// order into the packed system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2]; the
+// last of the blocks and norm chunks adds the norms and, with fuse_solve (single GPU), solves.
+// (One last-arriver assembling every block alone took ~56 us at m = 90.)
 constexpr int kSub = 5;
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
 __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
@@ -1658,7 +1660,6 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     const int tid = threadIdx.x;
     __shared__ double part[kSub][48];
     __shared__ double red[256];
-    __shared__ int last;
     if (item < a.n_items) {
         const int4 it = a.items[item];   // {block, begin, end, -}
         const int q = tid % 48, sub = tid / 48;
@@ -1696,7 +1697,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         if (tid < 48) {
             double t = part[0][tid];
             for (int c = 1; c < kSub; ++c) t += part[c][tid];
-            a.item_out[48 * (size_t)item + tid] = t;
+            st_sc1(a.item_out + 48 * (size_t)item + tid, t);
         }
     } else {
         const int c = item - a.n_items;
@@ -1708,79 +1709,69 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
                 if (tid < o) red[tid] += red[tid + o];
                 __syncthreads();
             }
-            if (tid == 0) a.item_out[48 * (size_t)item + w] = red[0];
+            if (tid == 0) st_sc1(a.item_out + 48 * (size_t)item + w, red[0]);
             __syncthreads();
         }
     }
     STAMPP(a.stamps, 8, 1);
-    // ---- publish the partial, take a ticket (agent-scope release/acquire, cdna guide G16)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int t = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (t == (int)gridDim.x - 1);
-    }
-    __syncthreads();
-    if (!last) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    STAMPP(a.stamps, 8, 2);
-    // ---- assemble (fixed order): S full into LDS, packed to global
-    extern __shared__ __attribute__((aligned(16))) double sm[];
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    // ---- level 1 (write-through hand-off, no fences): the last item of a camera-pair block sums
+    // the block's items in item order and writes the block's entries of the packed system
+    if (item < a.n_items) {
+        const int blk = a.items[item].x;
+        const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
+        if (!arrive_last_sc1(a.cnt_blk + blk, nk)) return;
+        if (tid < 48) {
+            int b1 = 0;
+            while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
+            const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
+            // unconditional loads (item_out is padded by kMaxItemsPerBlock zeroed items), masked adds
+            double pv[kMaxItemsPerBlock];
+#pragma unroll
+            for (int q = 0; q < kMaxItemsPerBlock; ++q) pv[q] = ld_sc1(a.item_out + 48 * (size_t)(k0 + q) + tid);
+            double v = 0.0;
+#pragma unroll
+            for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? pv[q] : 0.0;
+            if (tid < 36) {
+                const int ii = tid / 6, jj = tid % 6;
+                if (b1 != b2 || ii <= jj) st_sc1(a.packed + packed_index(6 * b1 + ii, 6 * b2 + jj, m), v);
+            } else if (b1 == b2) {
+                const int w = (tid - 36) / 6, i = 6 * b1 + (tid - 36) % 6;
+                st_sc1(a.packed + ntri + w * m + i, v);   // r (w = 0), JTE of the global block (w = 1)
+            }
+        }
+    }
+    STAMPP(a.stamps, 8, 2);
+    // ---- level 2: the last of the blocks and norm chunks adds the stop-test norms
+    if (!arrive_last_sc1(a.counter, a.nblk + (int)gridDim.x - a.n_items)) return;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;          // m*m
     double* r = sm + m * m;  // m
     __shared__ double norms[2];
-    for (int t = tid; t < ntri + 2 * m + 2; t += blockDim.x) {
+    if (tid < 2) {
+        const int w = tid;   // 0: normG2, 1: normX2 of the last update
         double v = 0.0;
-        if (t < ntri + 2 * m) {
-            int i, j, w = 0, blk;
-            const double* src;
-            if (t < ntri) {
-                packed_ij(t, m, i, j);
-                const int b1 = i / 6, b2 = j / 6;
-                blk = b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1);
-                src = a.item_out + (i % 6) * 6 + (j % 6);
-            } else {
-                const int u = t - ntri;
-                i = u % m; j = i; w = u / m;
-                const int b = i / 6;
-                blk = b * nb - b * (b - 1) / 2;
-                src = a.item_out + 36 + 6 * w + i % 6;
-            }
-            const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
-            // unconditional loads (item_out is padded by kMaxItemsPerBlock zeroed items), masked
-            // adds: no branch around the loads (cdna guide section 5, item 4(c))
-            double part[kMaxItemsPerBlock];
-#pragma unroll
-            for (int q = 0; q < kMaxItemsPerBlock; ++q) part[q] = src[48 * (size_t)(k0 + q)];
-#pragma unroll
-            for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? part[q] : 0.0;
-            if (t < ntri) {
-                S[i * m + j] = v;
-                S[j * m + i] = v;
-            } else if (w == 0) {
-                r[i] = v;
-            }
-        } else {
-            const int w = t - ntri - 2 * m;   // 0: normG2, 1: normX2 of the last update
-            if (st->iter > 0) {
-                for (int k = a.n_items; k < (int)gridDim.x; ++k) v += a.item_out[48 * (size_t)k + w];
-                if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
-            }
-            norms[w] = v;
+        if (st->iter > 0) {
+            for (int k = a.n_items; k < (int)gridDim.x; ++k) v += ld_sc1(a.item_out + 48 * (size_t)k + w);
+            if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
         }
-        a.packed[t] = v;
+        norms[w] = v;
+        a.packed[ntri + 2 * m + w] = v;
     }
     if (!a.fuse_solve) return;
-    __syncthreads();
     STAMPP(a.stamps, 8, 3);
+    for (int t = tid; t < ntri + m; t += blockDim.x) {
+        const double v = ld_sc1(a.packed + t);
+        if (t < ntri) {
+            int i, j;
+            packed_ij(t, m, i, j);
+            S[i * m + j] = v;
+            S[j * m + i] = v;
+        } else {
+            r[t - ntri] = v;
+        }
+    }
+    __syncthreads();
     SolveCtx sc = a.solve;
     sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
     solve_global<false>(sc, S, r, norms[0], norms[1]);
