@@ -17,6 +17,8 @@
 // latency bound.  All reductions are fixed-order, so a run is bitwise reproducible.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "mcc_device.hpp"
 #include "mcc_internal.h"
 
@@ -1558,6 +1560,186 @@ __device__ __forceinline__ void gj_tiled(const double* packed, double* r, int m,
     __syncthreads();
 }
 
+// Blocked Gauss-Jordan of [S | r] for m > 30 (m <= 128; k_solve), 16 x 16 blocks in LDS:
+// A = S padded with the identity to M = 16 nb rows (stride M + 1: odd, conflict-free columns),
+// x = r.  Per pivot block kb: (1) wave 0 inverts A[kb][kb] (register Gauss-Jordan, lane i owns
+// row i of [P | I]); (2) the pivot block row is scaled by the inverse, A[kb][j] <- P^-1 A[kb][j]
+// (j > kb) and x_kb <- P^-1 x_kb; (3) the block column is eliminated from every other block row,
+// A[i][j] -= A[i][kb] A[kb][j], x_i -= A[i][kb] x_kb.  Every 16 x 16 x 16 block product is four
+// v_mfma_f64_16x16x4_f64 (operands straight from LDS, items dealt round-robin to the 4 waves).
+// S is SPD: no pivoting.  x ends as the solution.
+typedef double v4f64_t __attribute__((ext_vector_type(4)));
+constexpr int kBlkLd = 17;   // stride of the 16 x 16 pivot-inverse scratch
+__device__ __forceinline__ int gjb_ld(int m) { return 16 * ((m + 15) / 16) + 1; }
+__device__ __forceinline__ void blk_mfma(double* C, int ldc, const double* Ap, int lda, const double* Bp, int ldb,
+                                         bool sub, bool zero_c) {
+    const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
+    v4f64_t acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = zero_c ? 0.0 : C[(kq + 4 * r) * ldc + i];
+    double av[4], bv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        av[q] = Ap[i * lda + 4 * q + kq];   // A[i][k], k = 4q + kq
+        bv[q] = Bp[(4 * q + kq) * ldb + i];  // B[k][j], j = i
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sub ? -av[q] : av[q], bv[q], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[(kq + 4 * r) * ldc + i] = acc[r];   // C[row = kq + 4r][col = i]
+}
+// 16 x 16 SPD inverse by one wave, all 64 lanes: lane l holds row i = l & 15, columns 8g .. 8g+7
+// (g = l >> 4) of [P | I].  Pivot k: its value by v_readlane, the pivot row's columns of every
+// lane by DPP row_newbcast:k inside each 16-lane row (the lanes of one column group), the
+// eliminated column entry of each row by one bpermute.  Columns left of the pivot in the P half are
+// left stale (never read).  Writes P^-1 to PV (stride kBlkLd); returns false if a pivot is not > 0.
+template <int K>
+__device__ __forceinline__ double gjb_bcast16(double v) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)u, 0x150 + K, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x150 + K, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int K>
+struct GjbStep {
+    __device__ __forceinline__ static void run(double (&v)[8], int lane, double& dii, bool& ok) {
+        constexpr int gk = K >> 3, ck = K & 7;
+        const double piv = readlane_f64(v[ck], K + 16 * gk);
+        ok &= piv > 0.0;
+        const double pv = piv > 0.0 ? piv : 1.0;
+        double ip = __builtin_amdgcn_rcp(pv);
+        ip = fma(ip, fma(-pv, ip, 1.0), ip);
+        const int i = lane & 15;
+        const double rik = __shfl(v[ck], i + 16 * gk);   // row i's column-K entry
+        const double f = i == K ? 0.0 : rik * ip;
+        if (i == K) dii = pv;
+        double pr[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pr[c] = gjb_bcast16<K>(v[c]);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] -= f * pr[c];
+        GjbStep<K + 1>::run(v, lane, dii, ok);
+    }
+};
+template <>
+struct GjbStep<16> {
+    __device__ __forceinline__ static void run(double (&)[8], int, double&, bool&) {}
+};
+__device__ __forceinline__ bool gjb_inverse16(const double* Pk, int ld, double* PV, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    double v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int col = 8 * g + c;
+        v[c] = col < 16 ? Pk[i * ld + (col < 16 ? col : 0)] : (col - 16 == i ? 1.0 : 0.0);
+    }
+    double dii = 1.0;
+    bool ok = true;
+    GjbStep<0>::run(v, lane, dii, ok);
+    if (g >= 2) {
+        const double id = 1.0 / dii;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) PV[i * kBlkLd + 8 * (g - 2) + c] = v[c] * id;
+    }
+    return ok;
+}
+#ifdef MCC_GJB_STAMPS
+__device__ long long g_gjb_stamps[64];
+#define GJB_STAMP(k) do { if (threadIdx.x == 0) g_gjb_stamps[k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define GJB_STAMP(k) do { } while (0)
+#endif
+__device__ __forceinline__ void gj_blocked(const double* packed, double* x, double* A, double* PV, int m, int* err) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int nb = (m + 15) / 16, M = 16 * nb, ld = M + 1, ntri = m * (m + 1) / 2;
+    // the packed upper triangle read contiguously (coalesced, 16 loads in flight per thread), each
+    // entry placed at (i, j) and (j, i); the identity padding of rows / columns >= m separately
+    constexpr int LB = 16;
+    for (int t0 = 0; t0 < ntri; t0 += LB * (int)blockDim.x) {
+        double v[LB];
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+            const int t = t0 + u * (int)blockDim.x + tid;
+            v[u] = packed[t < ntri ? t : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < LB; ++u) {
+            const int t = t0 + u * (int)blockDim.x + tid;
+            if (t >= ntri) continue;
+            // row i: first index i m - i (i - 1) / 2 <= t (quadratic estimate, then exact)
+            const float b = 2.0f * m + 1.0f;
+            int i = (int)((b - sqrtf(b * b - 8.0f * (float)t)) * 0.5f);
+            i = max(0, min(i, m - 1));
+            while (i > 0 && packed_index(i, i, m) > t) --i;
+            while (i + 1 < m && packed_index(i + 1, i + 1, m) <= t) ++i;
+            const int j = i + (t - packed_index(i, i, m));
+            A[i * ld + j] = v[u];
+            A[j * ld + i] = v[u];
+        }
+    }
+    for (int t = tid; t < M * M - m * m; t += blockDim.x) {   // padding: rows / columns m .. M-1
+        const int pad = M - m, ncol = pad * M;                 // t < ncol: rows m..M-1 (all columns)
+        int i, j;
+        if (t < ncol) { i = m + t / M; j = t % M; }
+        else { const int u = t - ncol; i = u / pad; j = m + u % pad; }   // rows < m, columns m..M-1
+        A[i * ld + j] = i == j ? 1.0 : 0.0;
+    }
+    for (int t = tid; t < M; t += blockDim.x) x[t] = t < m ? packed[ntri + t] : 0.0;
+    __syncthreads();
+    GJB_STAMP(0);
+    bool bad = false;
+    for (int kb = 0; kb < nb; ++kb) {
+        double* Pk = A + 16 * kb * ld + 16 * kb;
+        // (1) pivot block inverse: wave 0, all 64 lanes (gjb_inverse16)
+        if (wave == 0) bad |= !gjb_inverse16(Pk, ld, PV, lane);
+        __syncthreads();
+        GJB_STAMP(1 + 3 * kb);
+        // (2) scale the pivot block row: items j = kb+1 .. nb-1 (MFMA), then the rhs block
+        {
+            const int n2 = nb - 1 - kb;
+            for (int it = wave; it <= n2; it += nw) {
+                if (it < n2) {
+                    double* Ckj = A + 16 * kb * ld + 16 * (kb + 1 + it);
+                    blk_mfma(Ckj, ld, PV, kBlkLd, Ckj, ld, false, true);
+                } else {
+                    double v = 0.0;
+                    if (lane < 16) {
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) v += PV[lane * kBlkLd + k] * x[16 * kb + k];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < 16) x[16 * kb + lane] = v;
+                }
+            }
+        }
+        __syncthreads();
+        GJB_STAMP(2 + 3 * kb);
+        // (3) eliminate block column kb from the other block rows: items (ib, j), then the rhs
+        {
+            const int nj = nb - 1 - kb, n3 = (nb - 1) * nj;
+            for (int it = wave; it <= n3; it += nw) {
+                if (it < n3) {
+                    const int r = it / max(nj, 1), c = it % max(nj, 1);
+                    const int ib = r < kb ? r : r + 1, jb = kb + 1 + c;
+                    blk_mfma(A + 16 * ib * ld + 16 * jb, ld, A + 16 * ib * ld + 16 * kb, ld, A + 16 * kb * ld + 16 * jb, ld,
+                             true, false);
+                } else {
+                    for (int i = lane; i < M; i += 64) {
+                        if ((i >> 4) == kb) continue;
+                        double v = x[i];
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) v -= A[i * ld + 16 * kb + k] * x[16 * kb + k];
+                        x[i] = v;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        GJB_STAMP(3 + 3 * kb);
+    }
+    if (bad && lane == 0) atomicOr(err, 2);
+}
+
 __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err) {
     switch (m) {
 #define GJ(M) case M: gj_rows<M>(S, r, m, lane, err); break;
@@ -1606,11 +1788,9 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     __syncthreads();
     if (stop) return;
     SSTAMP(a.stamps, 4, 0);
-    if (LARGE) {   // S is the packed system itself (global), r the LDS output
-        if (m <= 48) gj_tiled<3, 4>(S, r, m, tid, &st->error);
-        else if (m <= 64) gj_tiled<4, 5>(S, r, m, tid, &st->error);
-        else if (m <= 96) gj_tiled<6, 7>(S, r, m, tid, &st->error);
-        else gj_tiled<8, 9>(S, r, m, tid, &st->error);
+    if (LARGE) {   // S is the packed system itself (global); r (LDS) is followed by the block work area
+        const int M = 16 * ((m + 15) / 16);
+        gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error);
     }
     SSTAMP(a.stamps, 5, 0);
     if (tid < 64) {
@@ -1786,8 +1966,8 @@ __global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
     double* S = sm;
     double* r = sm + m * m;
     if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed)) return;
-    if (m > 30) {   // the tiled elimination reads the packed system directly
-        solve_global<true>(a.ctx, a.packed, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+    if (m > 30) {   // the blocked elimination reads the packed system directly (LDS: x, A, pivot inverse)
+        solve_global<true>(a.ctx, a.packed, sm, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
         return;
     }
     for (int t = tid; t < ntri; t += blockDim.x) {
@@ -2039,7 +2219,11 @@ size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int 
     return fused ? std::max(lin, (size_t)(m * m + m) * sizeof(double)) : lin;
 }
 
-size_t mcc_solve_shmem(int m) { return (size_t)(m * m + m) * sizeof(double); }
+size_t mcc_solve_shmem(int m) {
+    const size_t M = 16 * (size_t)((m + 15) / 16);
+    const size_t blocked = M + M * (M + 1) + 16 * kBlkLd;   // gj_blocked (m > 30, k_solve)
+    return std::max((size_t)(m * m + m), m > 30 ? blocked : 0) * sizeof(double);
+}
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
     const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp);
@@ -2071,7 +2255,10 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int m
 }
 
 hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_schur, dim3(grid), dim3(256), mcc_solve_shmem(a.m), s, a);
+    // LDS for the solve only when this launch solves (single GPU, m <= 30): the item workgroups
+    // keep their occupancy
+    const size_t shm = a.fuse_solve ? (size_t)(a.m * a.m + a.m) * sizeof(double) : 0;
+    hipLaunchKernelGGL(k_schur, dim3(grid), dim3(256), shm, s, a);
     return hipGetLastError();
 }
 hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
