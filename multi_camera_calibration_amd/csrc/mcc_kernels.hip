@@ -1652,31 +1652,8 @@ __device__ long long g_gjb_stamps[64];
 __device__ __forceinline__ void gj_blocked(const double* packed, double* x, double* A, double* PV, int m, int* err) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int nb = (m + 15) / 16, M = 16 * nb, ld = M + 1, ntri = m * (m + 1) / 2;
-    // the packed upper triangle read contiguously (coalesced, 16 loads in flight per thread), each
-    // entry placed at (i, j) and (j, i); the identity padding of rows / columns >= m separately
-    constexpr int LB = 16;
-    for (int t0 = 0; t0 < ntri; t0 += LB * (int)blockDim.x) {
-        double v[LB];
-#pragma unroll
-        for (int u = 0; u < LB; ++u) {
-            const int t = t0 + u * (int)blockDim.x + tid;
-            v[u] = packed[t < ntri ? t : 0];
-        }
-#pragma unroll
-        for (int u = 0; u < LB; ++u) {
-            const int t = t0 + u * (int)blockDim.x + tid;
-            if (t >= ntri) continue;
-            // row i: first index i m - i (i - 1) / 2 <= t (quadratic estimate, then exact)
-            const float b = 2.0f * m + 1.0f;
-            int i = (int)((b - sqrtf(b * b - 8.0f * (float)t)) * 0.5f);
-            i = max(0, min(i, m - 1));
-            while (i > 0 && packed_index(i, i, m) > t) --i;
-            while (i + 1 < m && packed_index(i + 1, i + 1, m) <= t) ++i;
-            const int j = i + (t - packed_index(i, i, m));
-            A[i * ld + j] = v[u];
-            A[j * ld + i] = v[u];
-        }
-    }
+    // rhs, padding and the packed triangle: every global load is issued before the first LDS store
+    const double xr = tid < m ? packed[ntri + tid] : 0.0;   // M <= 128 <= blockDim.x
     for (int t = tid; t < M * M - m * m; t += blockDim.x) {   // padding: rows / columns m .. M-1
         const int pad = M - m, ncol = pad * M;                 // t < ncol: rows m..M-1 (all columns)
         int i, j;
@@ -1684,7 +1661,32 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
         else { const int u = t - ncol; i = u / pad; j = m + u % pad; }   // rows < m, columns m..M-1
         A[i * ld + j] = i == j ? 1.0 : 0.0;
     }
-    for (int t = tid; t < M; t += blockDim.x) x[t] = t < m ? packed[ntri + t] : 0.0;
+    // the packed upper triangle row by row (row i is contiguous from packed_index(i, i)): wave w
+    // takes rows w, w + 4, ..., twelve rows' loads in flight per lane; (i, j) and (j, i) written
+    constexpr int RB = 12;
+    for (int i0 = wave; i0 < m; i0 += RB * nw) {
+        double v[RB][2];
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {
+            const int i = min(i0 + q * nw, m - 1), base = packed_index(i, i, m), len = m - i;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) v[q][h] = packed[base + min(lane + 64 * h, len - 1)];
+        }
+#pragma unroll
+        for (int q = 0; q < RB; ++q) {
+            const int i = i0 + q * nw;
+            if (i >= m) continue;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j = i + lane + 64 * h;
+                if (j < m) {
+                    A[i * ld + j] = v[q][h];
+                    A[j * ld + i] = v[q][h];
+                }
+            }
+        }
+    }
+    if (tid < M) x[tid] = xr;
     __syncthreads();
     GJB_STAMP(0);
     bool bad = false;
