@@ -91,6 +91,26 @@ def setup_transport(ba, rank: int, world: int, same_device: bool) -> str:
     return "rccl"
 
 
+FP64_PEAK_TFS = 78.6   # MI355X FP64 vector peak, AMD spec
+
+
+def load_profile(prefix: str, config: str, n_views: int):
+    """The committed rocprofv3 --pmc result for this workload (profiles/<prefix>_*.json)."""
+    best = None
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for fn in sorted(os.listdir(pdir)):
+        if fn.startswith(prefix + "_") and fn.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(pdir, fn)))
+            except Exception:
+                continue
+            if d.get("config") == config and d.get("n_views") == n_views:
+                best = d
+    return best
+
+
 def load_traffic(config: str, n_views: int):
     """Per-launch HBM bytes of k_linearize from the committed rocprofv3 --pmc pass, if one
     exists for this workload (profiles/traffic_*.json, written by tools/pmc_traffic.py)."""
@@ -228,6 +248,14 @@ def main():
             "step_ms_events": step_ms_ev,
         },
     }
+    fp = load_profile("fp64", args.config, views_per_rank) if world == 1 else None
+    if fp and fp.get("fp64_flops_per_launch"):
+        tf = fp["fp64_flops_per_launch"] / (lin_ms * 1e-3) / 1e12
+        out["fp64_valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFS,
+                            "flops_per_launch": fp["fp64_flops_per_launch"],
+                            "flops_per_corner": fp["fp64_flops_per_corner"],
+                            "source": "profiles/fp64_*.json (rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, "
+                                      "an upper bound) / the event-timed launch"}
     if not args.no_parity and world == 1:
         from oracle import oracle_py as O
         o = O.Oracle(prob)

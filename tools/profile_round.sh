@@ -4,7 +4,8 @@
 #   2. rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE  -> memory-side bytes per launch
 #      (separate passes, kernel trace only: no sys/runtime tracing with --pmc)
 #   3. tools/pmc_traffic.py                              -> traffic_<config>_<views>.json
-#   4. the default bench.py line (with the traffic file in profiles/ so it is reported)
+#   4. rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 ...       -> fp64_<config>_<views>.json (tools/pmc_fp64.py)
+#   5. the default bench.py line (with both files in profiles/ so they are reported)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 TAG=${1:-r01}
@@ -27,6 +28,16 @@ ALG=$(python3 -c "import json; print([json.loads(l) for l in open('$OUT/stats.lo
 python3 tools/pmc_traffic.py --fetch "$OUT/pmc_fetch" --write "$OUT/pmc_write" --config config2 --views 500 \
     --alg-bytes "$ALG" --out "$OUT/traffic_config2_500.json" > "$OUT/traffic.log" 2>&1 || exit 15
 cp "$OUT/traffic_config2_500.json" profiles/ || exit 16
+cd /tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FMA_F64 \
+    SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 -d "$OUT/pmc_fp64" -o run --output-format csv \
+    -- python3 "$R/bench.py" --steps 40 --warmup 4 --no-cpu --no-parity > "$OUT/fp64.log" 2>&1 || exit 18
+echo "fp64 pass done"
+cd "$R"
+CORNERS=$(python3 -c "import json; print([json.loads(l) for l in open('$OUT/stats.log') if l.startswith('{\"metric')][-1]['config']['corners_per_step'])") || exit 19
+python3 tools/pmc_fp64.py --dir "$OUT/pmc_fp64" --config config2 --views 500 --corners "$CORNERS" \
+    --out "$OUT/fp64_config2_500.json" > "$OUT/fp64_tool.log" 2>&1 || exit 20
+cp "$OUT/fp64_config2_500.json" profiles/ || exit 21
 timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 17
 echo "bench done"
 cat "$OUT/bench.json"
