@@ -1596,8 +1596,9 @@ __device__ __forceinline__ void blk_mfma(double* C, int ldc, const double* Ap, i
 template <int K>
 __device__ __forceinline__ double gjb_bcast16(double v) {
     const long long u = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)u, 0x150 + K, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x150 + K, 0xF, 0xF, false);
+    // all rows / banks enabled: every lane is written, so no 'old' operand needs materialising
+    const int lo = __builtin_amdgcn_mov_dpp((int)u, 0x150 + K, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + K, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 template <int K>
@@ -1690,24 +1691,26 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
     __syncthreads();
     GJB_STAMP(0);
     bool bad = false;
+    // (1) pivot block inverse of block 0; later pivots are inverted one step ahead (look-ahead):
+    // in step kb, wave 0 first eliminates block (kb+1, kb+1) and inverts it while waves 1..3
+    // eliminate the rest; PV holds two 16 x 17 buffers (step parity)
+    if (wave == 0) bad |= !gjb_inverse16(A, ld, PV, lane);
+    __syncthreads();
     for (int kb = 0; kb < nb; ++kb) {
-        double* Pk = A + 16 * kb * ld + 16 * kb;
-        // (1) pivot block inverse: wave 0, all 64 lanes (gjb_inverse16)
-        if (wave == 0) bad |= !gjb_inverse16(Pk, ld, PV, lane);
-        __syncthreads();
         GJB_STAMP(1 + 3 * kb);
+        const double* PVk = PV + (kb & 1) * 16 * kBlkLd;
         // (2) scale the pivot block row: items j = kb+1 .. nb-1 (MFMA), then the rhs block
         {
             const int n2 = nb - 1 - kb;
             for (int it = wave; it <= n2; it += nw) {
                 if (it < n2) {
                     double* Ckj = A + 16 * kb * ld + 16 * (kb + 1 + it);
-                    blk_mfma(Ckj, ld, PV, kBlkLd, Ckj, ld, false, true);
+                    blk_mfma(Ckj, ld, PVk, kBlkLd, Ckj, ld, false, true);
                 } else {
                     double v = 0.0;
                     if (lane < 16) {
 #pragma unroll
-                        for (int k = 0; k < 16; ++k) v += PV[lane * kBlkLd + k] * x[16 * kb + k];
+                        for (int k = 0; k < 16; ++k) v += PVk[lane * kBlkLd + k] * x[16 * kb + k];
                     }
                     __builtin_amdgcn_wave_barrier();
                     if (lane < 16) x[16 * kb + lane] = v;
@@ -1719,7 +1722,9 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
         // (3) eliminate block column kb from the other block rows: items (ib, j), then the rhs
         {
             const int nj = nb - 1 - kb, n3 = (nb - 1) * nj;
-            for (int it = wave; it <= n3; it += nw) {
+            const bool ahead = kb + 1 < nb && nw > 1;
+            const int it0 = kb * nj;   // item of block (kb+1, kb+1): row index r = kb, column c = 0
+            auto item = [&](int it) {
                 if (it < n3) {
                     const int r = it / max(nj, 1), c = it % max(nj, 1);
                     const int ib = r < kb ? r : r + 1, jb = kb + 1 + c;
@@ -1734,6 +1739,15 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
                         x[i] = v;
                     }
                 }
+            };
+            if (!ahead) {
+                for (int it = wave; it <= n3; it += nw) item(it);
+            } else if (wave == 0) {
+                item(it0);
+                const int kn = kb + 1;
+                bad |= !gjb_inverse16(A + 16 * kn * ld + 16 * kn, ld, PV + (kn & 1) * 16 * kBlkLd, lane);
+            } else {
+                for (int q = wave - 1; q < n3; q += nw - 1) item(q < it0 ? q : q + 1);   // n3 - 1 blocks + rhs
             }
         }
         __syncthreads();
@@ -2223,7 +2237,7 @@ size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int 
 
 size_t mcc_solve_shmem(int m) {
     const size_t M = 16 * (size_t)((m + 15) / 16);
-    const size_t blocked = M + M * (M + 1) + 16 * kBlkLd;   // gj_blocked (m > 30, k_solve)
+    const size_t blocked = M + M * (M + 1) + 2 * 16 * kBlkLd;   // gj_blocked (m > 30, k_solve)
     return std::max((size_t)(m * m + m), m > 30 ? blocked : 0) * sizeof(double);
 }
 

@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(dp, packed.data(), sizeof(double) * packed.size(), hipMemcpyHostToDevice);
     (void)hipMemset(de, 0, sizeof(int));
     const int M = 16 * ((m + 15) / 16);
-    const size_t shm = sizeof(double) * (M + M * (M + 1) + 16 * mcc::kBlkLd);
+    const size_t shm = sizeof(double) * (M + M * (M + 1) + 2 * 16 * mcc::kBlkLd);
     (void)hipFuncSetAttribute((const void*)k_solve_bench, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
@@ -101,10 +101,10 @@ int main(int argc, char** argv) {
     long long st[64];
     (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(mcc::g_gjb_stamps), sizeof(st));
     const int nb = (m + 15) / 16;
-    std::printf("  load %lld  end-of-last-step -> kernel rep end n/a\n", st[0] - st[63]);
+    std::printf("  load %lld  first pivot %lld\n", st[0] - st[63], st[1] - st[0]);
     for (int kb = 0; kb < nb; ++kb)
-        std::printf("  kb %d: pivot-inverse %lld  scale-row %lld  eliminate %lld\n", kb, st[1 + 3 * kb] - st[3 * kb],
-                    st[2 + 3 * kb] - st[1 + 3 * kb], st[3 + 3 * kb] - st[2 + 3 * kb]);
+        std::printf("  kb %d: scale-row %lld  eliminate(+next pivot) %lld\n", kb, st[2 + 3 * kb] - st[1 + 3 * kb],
+                    st[3 + 3 * kb] - st[2 + 3 * kb]);
 #endif
     std::printf("m=%d %s err=%d median_ticks=%lld min=%lld rel_err=%.3e  kernel %.1f us for %d solves (%.2f us each)\n", m,
                 hipGetErrorString(e), err, t[REPS / 2], t[0], emax / xmax, ms * 1e3, REPS, ms * 1e3 / REPS);
