@@ -1,20 +1,26 @@
 // mcc_kernels.hip -- CDNA4 (gfx950) kernels of one Gauss-Newton step of the reference's
 // multi-camera extrinsic BA (MultiCameraCalibration::optimizeExtrinsics, src/multicalib.cpp:462-514).
 //
-// Step dataflow, single GPU = 2 launches:
+// Step dataflow:
 //   k_linearize   one workgroup per photo vertex, one wavefront per edge (camera observing it):
-//                 [pending photo update of the previous step: back-substitution + float32
-//                 update, fused here], edge prologue (compose_motion + fl32 pose, one lane per
-//                 edge), corner sweep (lanes over corners, FP64 projection + 2x6 Jacobian strips,
-//                 float32 residual), butterfly reduce-scatter of the 27 normal-equation sums,
-//                 chain rule to the photo / global blocks, 6x6 photo Cholesky, Y_e = H_gp L^-T.
-//   k_schur       work items of camera-pair blocks of S = sum H_gg - sum Y_e Y_e'^T and r, plus
-//                 norm chunks; the last-arriving workgroup assembles the packed system in fixed
-//                 order and (single GPU) solves it: stop test, Cholesky, global-block update.
-//   multi-GPU:    k_schur assembles only -> RCCL all-reduce of the packed system -> k_solve.
+//                 [pending photo update of the previous step, fused here], edge prologue
+//                 (compose_motion + fl32 pose), corner sweep (lanes over corners, FP64 projection
+//                 + 2x6 Jacobian strips, float32 residual), VALU butterfly reduce-scatter of the
+//                 27 normal-equation sums, chain rule to the photo / global blocks, 6x6 photo
+//                 inverse (register Gauss-Jordan), Schur factors Y'_e.
+//                 m <= 30 (single GPU): the WHOLE step is this one kernel -- per-photo packed
+//                 contributions, a two-level write-through last-arriver reduction, and the final
+//                 arriver's stop test + reduced solve + camera update (multi-GPU: with the
+//                 in-kernel peer exchange of the packed system first).
+//   k_schur       m > 30 (or RCCL): camera-pair-block work items of S = sum H_gg - sum Y' H_gp^T
+//                 and r, plus norm chunks; two-level write-through hand-off into the packed system.
+//   k_solve       m > 30 / RCCL: [peer exchange], stop test, blocked Gauss-Jordan (16 x 16 blocks,
+//                 MFMA f64 block products, look-ahead pivot inverses), camera update.
 //   k_backsub     standalone photo back-substitution (flush of a pending update / deltaX output).
-// No MFMA: the largest dense block is 6x6; the path is FP64-VALU and
-// latency bound.  All reductions are fixed-order, so a run is bitwise reproducible.
+//   k_project_error  computeProjectError's per-edge float32 sums.
+// The per-corner and per-edge blocks are at most 6x6: FP64 VALU, latency
+// bound; MFMA appears only in the large-m reduced solve.  All reductions are fixed-order, so a run
+// is bitwise reproducible.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1477,87 +1483,8 @@ __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int l
 }
 
 
-// Gauss-Jordan of [S | r] for m > 30 (m <= 128) by the whole workgroup with the matrix in
-// registers: thread (ti, tj) of a 16 x 16 grid owns rows ti + 16 a (a < R) and columns
-// tj + 16 b (b < CC, column m = r), loaded straight from the packed upper triangle.  Pivot
-// k = 16 ka + kr is owned by register slot ka (compile-time: the ka loop is unrolled), and
-// column slots b < ka lie left of every pivot of that block (skipped at compile time).  Per
-// pivot only its column and row travel through LDS (double-buffered: one barrier per step).
-// S is SPD: no pivoting.  Writes delta_i = r_i / S_ii into r[] (LDS).
 __device__ __forceinline__ int packed_index(int i, int j, int m) {   // i <= j
     return i * m - i * (i - 1) / 2 + (j - i);
-}
-template <int R, int CC>
-__device__ __forceinline__ void gj_tiled(const double* packed, double* r, int m, int tid, int* err) {
-    __shared__ double colb[2][128], rowb[2][136], pivs[128];
-    const int ti = tid >> 4, tj = tid & 15, ntri = m * (m + 1) / 2;
-    double A[R][CC];
-#pragma unroll
-    for (int a = 0; a < R; ++a) {
-        const int i = ti + 16 * a;
-#pragma unroll
-        for (int b = 0; b < CC; ++b) {
-            const int j = tj + 16 * b;
-            const bool ok = i < m && j <= m;
-            const int ic = ok ? i : 0, jc = ok ? j : 0;
-            const int idx = jc == m ? ntri + ic : (ic <= jc ? packed_index(ic, jc, m) : packed_index(jc, ic, m));
-            const double v = packed[idx];
-            A[a][b] = ok ? v : 0.0;
-        }
-    }
-    bool bad = false;
-#pragma unroll
-    for (int ka = 0; ka < CC; ++ka) {
-        if (16 * ka >= m) break;
-        const int kend = min(16, m - 16 * ka);
-        for (int kr = 0; kr < kend; ++kr) {
-            const int k = 16 * ka + kr, kb = k & 1;
-            if (ka < R && tj == kr) {   // owners of column k (slot ka) publish it
-#pragma unroll
-                for (int a = 0; a < R; ++a)
-                    if (ti + 16 * a < m) colb[kb][ti + 16 * a] = A[a][ka];
-            }
-            if (ka < R && ti == kr) {   // owners of row k (slot ka) publish it
-#pragma unroll
-                for (int b = ka; b < CC; ++b)
-                    if (tj + 16 * b <= m) rowb[kb][tj + 16 * b] = A[ka][b];
-            }
-            __syncthreads();
-            const double piv = rowb[kb][k];
-            if (tid == 0) pivs[k] = piv;
-            bad |= !(piv > 0.0);
-            const double pv = piv > 0.0 ? piv : 1.0;
-            double ip = __builtin_amdgcn_rcp(pv);
-            ip = fma(ip, fma(-pv, ip, 1.0), ip);
-            double rk[CC];
-#pragma unroll
-            for (int b = ka; b < CC; ++b) {
-                const int j = tj + 16 * b;
-                rk[b] = ((b > ka || tj > kr) && j <= m) ? rowb[kb][j <= m ? j : m] : 0.0;
-            }
-#pragma unroll
-            for (int a = 0; a < R; ++a) {
-                const int i = ti + 16 * a;
-                const double f = (i < m && i != k) ? colb[kb][i < m ? i : 0] * ip : 0.0;
-#pragma unroll
-                for (int b = ka; b < CC; ++b) A[a][b] -= f * rk[b];
-            }
-        }
-    }
-    __syncthreads();
-    if (tj == (m & 15)) {
-        const int bm = m >> 4;
-#pragma unroll
-        for (int a = 0; a < R; ++a) {
-            const int i = ti + 16 * a;
-            double v = 0.0;
-#pragma unroll
-            for (int b = 0; b < CC; ++b) v = b == bm ? A[a][b] : v;
-            if (i < m) r[i] = v / pivs[i];
-        }
-    }
-    if (bad && tid == 0) atomicOr(err, 2);
-    __syncthreads();
 }
 
 // Blocked Gauss-Jordan of [S | r] for m > 30 (m <= 128; k_solve), 16 x 16 blocks in LDS:
