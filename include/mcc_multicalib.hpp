@@ -155,6 +155,23 @@ public:
           timestampAvailable(nCameras), _omEachCamera(nCameras), _tEachCamera(nCameras) {
         for (int c = 0; c < nCameras; ++c) _vertexList.emplace_back(eye4(), -1);   // camera vertices
     }
+    // the reference's constructor (multicalib.hpp:138-143) minus the feature detector / descriptor /
+    // matcher (image feature matching is out of scope): fileName names an imagelist_creator list
+    // whose entries after the first (the pattern) are per-view corner files "cameraIdx-timestamp.*"
+    // read by loadImages(); TermCriteria defaults to the reference's (COUNT, 20, 1e-7)
+    MultiCameraCalibration(int cameraType, int nCameras, const std::string& fileName, float patternWidth,
+                           float patternHeight, int verbose = 0, int showExtration = 0, int nMiniMatches = 20,
+                           int flags = 0, TermCriteria criteria = TermCriteria(TermCriteria::COUNT, 20, 1e-7),
+                           int device = 0)
+        : MultiCameraCalibration(cameraType, nCameras, criteria, device) {
+        _filename = fileName;
+        _patternWidth = patternWidth;
+        _patternHeight = patternHeight;
+        _verbose = verbose;
+        _showExtraction = showExtration;
+        _nMiniMatches = nMiniMatches;
+        _flags = flags;
+    }
     virtual ~MultiCameraCalibration() { release(); }
     MultiCameraCalibration(const MultiCameraCalibration&) = delete;
     MultiCameraCalibration& operator=(const MultiCameraCalibration&) = delete;
@@ -175,9 +192,16 @@ public:
     // ---- the sample's driver (libmcc_host.so)
     // loadImages + initialize + optimizeExtrinsics (src/multicalib.cpp:127-133)
     virtual double run();
-    // the base class's random-pattern loader is out of scope (feature matching on images):
-    // throws; MyMultiCameraCalibration::loadImages reads pre-detected corners
+    // loadImages (src/multicalib.cpp:182-321) on pre-detected corners: the random-pattern feature
+    // matching on images is out of scope, so each list entry "cameraIdx-timestamp.*" names a corner
+    // file (an image name maps to <stem>.yaml beside it) holding imagePoints (N x 2 or N x 1 x 2),
+    // objectPoints (N x 3 or N x 1 x 3) and imageSize; views with more than nMiniMatches points are
+    // kept; OMNIDIRECTIONAL cameras are calibrated with cv::omnidir::calibrate on the GPU
+    // (mcc_omnidir.hpp, TermCriteria(COUNT + EPS, 300, 1e-7), flags), PINHOLE would need
+    // cv::calibrateCamera (not restated: throws); the calibration's view poses become the edges
     virtual void loadImages();
+    // readStringList (src/multicalib.cpp:167-180): the strings of the list file's first node
+    std::vector<std::string> readStringList() const;
     // graph BFS from camera 0 and pose chaining (src/mymulticalib.cpp:615-666)
     virtual void initialize();
     // reset (src/multicalib.cpp:134-152): clears the edges, the photo vertices and the per-camera
@@ -270,6 +294,9 @@ public:
     std::vector<float> _xi;                                                    // Mei xi (omnidirectional)
     double _error = 0.0;                                                       // meanReprojectError
     int _verbose = 0;
+    std::string _filename;                                                     // the image / corner-file list
+    float _patternWidth = 0.f, _patternHeight = 0.f;
+    int _nMiniMatches = 20, _flags = 0, _showExtraction = 0;
     // per camera, per stored view (loadImages): file, timestamp, solvePnP pose
     std::vector<std::vector<std::string>> filesEachCameraFull;
     std::vector<std::vector<int>> timestampFull, timestampAvailable;

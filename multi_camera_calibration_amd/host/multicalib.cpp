@@ -13,6 +13,7 @@
 #include <iostream>
 
 #include "mcc_multicalib.hpp"
+#include "mcc_omnidir.hpp"
 #include "mcc_pnp.hpp"
 #include "mcc_storage.hpp"
 
@@ -94,10 +95,107 @@ double MultiCameraCalibration::run() {
     return optimizeExtrinsics();
 }
 
+std::vector<std::string> MultiCameraCalibration::readStringList() const {
+    stg::FileStorage fs(_filename, stg::FileStorage::READ);
+    if (!fs.isOpened()) throw std::runtime_error("cannot read the image list " + _filename);
+    const std::vector<std::string> keys = fs.keys();
+    if (keys.empty()) throw std::runtime_error(_filename + ": empty image list");
+    const stg::Node& n = fs[keys[0]];   // getFirstTopLevelNode
+    std::vector<std::string> l;
+    for (const stg::Node& k : n.seq) {
+        if (k.type != stg::Node::STRING) throw std::runtime_error(_filename + ": list entries must be file names");
+        l.push_back(k.str);
+    }
+    return l;
+}
+
 void MultiCameraCalibration::loadImages() {
-    throw std::runtime_error(
-        "MultiCameraCalibration::loadImages: random-pattern feature matching on images is out of scope; use "
-        "MyMultiCameraCalibration (pre-detected corner files) or fill the state directly");
+    namespace fsys = std::filesystem;
+    const std::vector<std::string> file_list = readStringList();
+    if (file_list.size() < 2) throw std::runtime_error(_filename + ": the list holds no view after the pattern");
+    const fsys::path base = fsys::path(_filename).parent_path();
+    // entry 0 is the pattern image (only the feature matcher reads it); the others are
+    // "cameraIdx-timestamp.*" (src/multicalib.cpp:199-218)
+    for (size_t i = 1; i < file_list.size(); ++i) {
+        fsys::path f(file_list[i]);
+        if (f.is_relative() && !base.empty() && !fsys::exists(f)) f = base / f;
+        const std::string ext = f.extension().string();
+        if (ext != ".yaml" && ext != ".yml" && ext != ".xml") f.replace_extension(".yaml");   // image -> its corners
+        int cameraVertex = -1, timestamp = 0;
+        if (std::sscanf(f.stem().string().c_str(), "%d-%d", &cameraVertex, &timestamp) != 2 || cameraVertex < 0 ||
+            cameraVertex >= _nCamera)
+            throw std::runtime_error(file_list[i] + ": expected a 'cameraIdx-timestamp' name with cameraIdx < " +
+                                     std::to_string(_nCamera));
+        filesEachCameraFull[cameraVertex].push_back(f.string());
+        timestampFull[cameraVertex].push_back(timestamp);
+    }
+    for (int camera = 0; camera < _nCamera; ++camera) {   // calibrate each camera individually
+        Size size;
+        std::vector<std::vector<mcc::omnidir::Vec3d>> objs;
+        std::vector<std::vector<mcc::omnidir::Vec2d>> imgs;
+        for (size_t imgIdx = 0; imgIdx < filesEachCameraFull[camera].size(); ++imgIdx) {
+            const std::string& file = filesEachCameraFull[camera][imgIdx];
+            stg::FileStorage fs(file, stg::FileStorage::READ);
+            if (!fs.isOpened()) throw std::runtime_error("cannot read " + file);
+            const bool tut = !fs["imagePoints"].empty();
+            const std::vector<double> img = points_of(fs[tut ? "imagePoints" : "corners"], 2, file, "imagePoints");
+            const std::vector<double> obj = points_of(fs[tut ? "objectPoints" : "objects"], 3, file, "objectPoints");
+            const int n = (int)img.size() / 2;
+            if ((int)obj.size() != 3 * n) throw std::runtime_error(file + ": image and object points differ in count");
+            const stg::Node& sz = fs["imageSize"];
+            if (sz.seq.size() == 2) size = Size(sz.seq[0].toInt(), sz.seq[1].toInt());   // image.size()
+            if (n > _nMiniMatches) {   // (int)imgObj[0].total() > _nMiniMatches
+                std::vector<float> fi(img.size()), fo(obj.size());   // the finder's CV_32F points
+                for (size_t k = 0; k < img.size(); ++k) fi[k] = (float)img[k];
+                for (size_t k = 0; k < obj.size(); ++k) fo[k] = (float)obj[k];
+                std::vector<mcc::omnidir::Vec3d> o3(n);
+                std::vector<mcc::omnidir::Vec2d> i2(n);
+                for (int k = 0; k < n; ++k) {   // calibrate converts CV_32F to CV_64F
+                    o3[k] = {(double)fo[3 * k], (double)fo[3 * k + 1], (double)fo[3 * k + 2]};
+                    i2[k] = {(double)fi[2 * k], (double)fi[2 * k + 1]};
+                }
+                objs.push_back(std::move(o3));
+                imgs.push_back(std::move(i2));
+                _imagePointsForEachCamera[camera].push_back(std::move(fi));
+                _objectPointsForEachCamera[camera].push_back(std::move(fo));
+                timestampAvailable[camera].push_back(timestampFull[camera][imgIdx]);
+            } else if (_verbose) {
+                std::cout << "image " << file << " has too few matched points " << std::endl;
+            }
+        }
+        if (objs.empty()) throw std::runtime_error("camera " + std::to_string(camera) + " has no usable view");
+        if (size.width <= 0 || size.height <= 0)
+            throw std::runtime_error("camera " + std::to_string(camera) + ": no imageSize in its corner files");
+        if (_camType != OMNIDIRECTIONAL)
+            throw std::runtime_error(
+                "MultiCameraCalibration::loadImages: PINHOLE intrinsics need cv::calibrateCamera, which is not "
+                "restated here; use MyMultiCameraCalibration with camera configs");
+        std::array<double, 9> K{};
+        std::array<double, 4> D{};
+        double xi = 0;
+        std::vector<mcc::omnidir::Vec3d> om, t;
+        std::vector<int> idx;
+        const double rms = mcc::omnidir::calibrate(objs, imgs, size, K, xi, D, om, t, _flags,
+                                                   TermCriteria(TermCriteria::COUNT + TermCriteria::EPS, 300, 1e-7),
+                                                   &idx, _device);
+        for (int k = 0; k < 9; ++k) _cameraMatrix[camera][k] = (float)K[k];   // convertTo(CV_32F)
+        _distortCoeffs[camera].assign({(float)D[0], (float)D[1], (float)D[2], (float)D[3]});
+        _xi[camera] = (float)xi;
+        for (size_t i = 0; i < om.size(); ++i) {   // edges from the calibration's view poses (:296-312)
+            const std::array<float, 3> r{(float)om[i][0], (float)om[i][1], (float)om[i][2]};
+            const std::array<float, 3> tv{(float)t[i][0], (float)t[i][1], (float)t[i][2]};
+            _omEachCamera[camera].push_back(r);
+            _tEachCamera[camera].push_back(tv);
+            const int timestamp = timestampAvailable[camera][idx[i]];
+            const int photoVertex = getPhotoVertex(timestamp);
+            _edgeList.push_back(edge(camera, photoVertex, idx[i], rt_to_pose(r.data(), tv.data())));
+        }
+        if (_verbose) {
+            std::cout << "initialized for camera " << camera << " rms = " << rms << std::endl;
+            std::cout << "xi for camera " << camera << " is " << _xi[camera] << std::endl;
+        }
+    }
+    release();
 }
 
 void MultiCameraCalibration::graphTraverse(int begin, std::vector<int>& order, std::vector<int>& pre,

@@ -91,6 +91,46 @@ Node scalar_node(const std::string& text) {
     return n;
 }
 
+// a whitespace / comma separated list ('[' ']' allowed) of numbers, or of (quoted) strings such as
+// imagelist_creator's image names: REAL nodes when every token is a number, STRING nodes otherwise
+Node list_node(const std::string& text) {
+    std::vector<std::string> toks;
+    std::string cur;
+    bool quoted = false;
+    for (char c : text) {
+        if (c == '"') {
+            quoted = !quoted;
+            cur += c;
+        } else if (!quoted && (std::isspace((unsigned char)c) || c == ',' || c == '[' || c == ']')) {
+            if (!cur.empty()) toks.push_back(cur);
+            cur.clear();
+        } else {
+            cur += c;
+        }
+    }
+    if (!cur.empty()) toks.push_back(cur);
+    bool numeric = true;
+    for (const std::string& t : toks) {
+        char* end = nullptr;
+        std::strtod(t.c_str(), &end);
+        numeric = numeric && end && *end == '\0' && !t.empty();
+    }
+    Node n;
+    n.type = Node::SEQ;
+    for (const std::string& t : toks) {
+        Node k;
+        if (numeric) {
+            k.type = Node::REAL;
+            k.real = std::strtod(t.c_str(), nullptr);
+        } else {
+            k.type = Node::STRING;
+            k.str = unquote(t);
+        }
+        n.seq.push_back(k);
+    }
+    return n;
+}
+
 Node make_mat(int rows, int cols, const std::string& dt, const std::string& data) {
     Node n;
     n.type = Node::MAT;
@@ -211,17 +251,9 @@ Node xml_node(const XmlElem& e) {
         return n;
     }
     const std::string t = trim(e.text);
-    if (t.find(' ') != std::string::npos && t.front() != '"') {   // a whitespace-separated number list
-        Node n;
-        n.type = Node::SEQ;
-        for (double v : parse_numbers(t)) {
-            Node k;
-            k.type = Node::REAL;
-            k.real = v;
-            n.seq.push_back(k);
-        }
-        return n;
-    }
+    if (t.find_first_of(" \n\t") != std::string::npos && !(t.front() == '"' && t.back() == '"' &&
+                                                          t.find('"', 1) == t.size() - 1))
+        return list_node(t);   // a whitespace-separated list of numbers or strings
     return scalar_node(t);
 }
 
@@ -292,17 +324,7 @@ private:
     }
     Node value(const std::string& rest, int indent) {
         if (rest.rfind("!!opencv-matrix", 0) == 0) return mapping_mat(indent);
-        if (!rest.empty() && rest[0] == '[') {
-            Node n;
-            n.type = Node::SEQ;
-            for (double v : parse_numbers(bracket(rest))) {
-                Node k;
-                k.type = Node::REAL;
-                k.real = v;
-                n.seq.push_back(k);
-            }
-            return n;
-        }
+        if (!rest.empty() && rest[0] == '[') return list_node(bracket(rest));
         if (!rest.empty()) return scalar_node(rest);
         // block sequence: "- item" lines deeper than (or at) the key's indent
         Node n;

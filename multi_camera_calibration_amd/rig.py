@@ -488,17 +488,20 @@ class OmniCalibViews:
 
 
 def make_omni_views(n_views=1000, board=(11, 8), square=40.0, seed=4, noise_px=0.2,
-                    size=(1280, 960)) -> OmniCalibViews:
-    """Mei-model camera (config 4's intrinsics: f ~ 350, xi ~ U(0.8, 1.2), 1280x960, D = 4) and
-    n_views board poses 350-1300 mm away, up to 55 deg off axis, tilted up to 45 deg, every corner
-    inside the image with a 20 px margin; 0.2 px Gaussian corner noise."""
+                    size=(1280, 960), K=None, xi=None, D=None) -> OmniCalibViews:
+    """Mei-model camera (config 4's intrinsics: f ~ 350, xi ~ U(0.8, 1.2), 1280x960, D = 4; or the
+    given K / xi / D) and n_views board poses 350-1300 mm away, up to 55 deg off axis, tilted up to
+    45 deg, every corner inside the image with a 20 px margin; 0.2 px Gaussian corner noise."""
     rng = np.random.default_rng(seed)
     W, H = size
     f = 350.0 * rng.uniform(0.97, 1.03)
-    K = np.array([[f, 0.0, W / 2 + rng.uniform(-10, 10)], [0, f * rng.uniform(0.99, 1.01), H / 2 + rng.uniform(-10, 10)],
-                  [0, 0, 1]])
-    xi = float(rng.uniform(0.8, 1.2))
-    D = np.array([rng.uniform(-0.1, 0.0), rng.uniform(0.0, 0.05), rng.uniform(-5e-4, 5e-4), rng.uniform(-5e-4, 5e-4)])
+    K0 = np.array([[f, 0.0, W / 2 + rng.uniform(-10, 10)], [0, f * rng.uniform(0.99, 1.01), H / 2 + rng.uniform(-10, 10)],
+                   [0, 0, 1]])
+    xi0 = float(rng.uniform(0.8, 1.2))
+    D0 = np.array([rng.uniform(-0.1, 0.0), rng.uniform(0.0, 0.05), rng.uniform(-5e-4, 5e-4), rng.uniform(-5e-4, 5e-4)])
+    K = K0 if K is None else np.asarray(K, np.float64)
+    xi = xi0 if xi is None else float(xi)
+    D = D0 if D is None else np.asarray(D, np.float64)
     pts = board_points(board[0], board[1], square)
     ctr = pts.mean(0)
     oms, ts, imgs = [], [], []

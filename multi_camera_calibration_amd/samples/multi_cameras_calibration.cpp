@@ -12,6 +12,13 @@
 // camera poses from the configs' CameraMatrix, the double-side transform optimised; its
 // writeParameters writes doublesideTransform.yaml in the working directory).
 //
+// --list FILE runs the base MultiCameraCalibration instead, as the reference's multi-camera
+// tutorial does (tutorials/multi_camera_tutorial.markdown: construct, run(), writeParameters):
+// FILE is an imagelist_creator list whose entries after the first are per-view corner files
+// "cameraIdx-timestamp.yaml" (imagePoints, objectPoints, imageSize); with --omni (the only camera
+// type whose intrinsics are restated) every camera is first calibrated by cv::omnidir::calibrate
+// on the GPU.  --cameras N (required), --min-matches K (nMiniMatches, default 20).
+//
 // --init-only stops after loadImages + initialize (no GPU needed).  --dump-problem writes the
 // problem of the last pass (tests/cpp blob format + photo timestamps) with x0 = buildParas(),
 // --dump-result the optimised parameters, error, iterations and the outlier files.
@@ -49,7 +56,7 @@ void wr(std::ofstream& f, const T* p, size_t n) {
 }
 
 // the problem as the C ABI sees it (edge order, photo index = vertex - C), x0 = buildParas()
-void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
+void dump_problem(MultiCameraCalibration& mc, const std::string& path) {
     const int C = mc._nCamera, V = (int)mc._vertexList.size() - C, E = (int)mc._edgeList.size();
     const int nd = (int)mc._distortCoeffs[0].size();
     std::vector<int> ecam, ephoto, eside, eoff, en;
@@ -68,10 +75,13 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
         corners += (int)o.size() / 3;
     }
     auto* dsc = dynamic_cast<DoubleSideCalibration*>(&mc);
+    auto* my = dynamic_cast<MyMultiCameraCalibration*>(&mc);
     bool has_ds = false;
-    if (!dsc)
-        for (double v : mc.doubleSideTransform) has_ds = has_ds || v != 0.0;
-    const int hdr[11] = {0x4d434331, dsc ? MCC_MODEL_DOUBLESIDE : MCC_MODEL_PINHOLE, C, V, E, nd, corners,
+    if (!dsc && my)
+        for (double v : my->doubleSideTransform) has_ds = has_ds || v != 0.0;
+    const int model = dsc ? MCC_MODEL_DOUBLESIDE
+                          : (mc._camType == MultiCameraCalibration::OMNIDIRECTIONAL ? MCC_MODEL_OMNI : MCC_MODEL_PINHOLE);
+    const int hdr[11] = {0x4d434331, model, C, V, E, nd, corners,
                          has_ds ? 1 : 0, dsc ? 1 : 0, mc._criteria.type, mc._criteria.maxCount};
     std::ofstream f(path, std::ios::binary);
     wr(f, hdr, 11);
@@ -82,7 +92,7 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
     for (int c = 0; c < C; ++c) wr(f, mc._cameraMatrix[c].data(), 9);
     for (int c = 0; c < C; ++c) wr(f, mc._distortCoeffs[c].data(), nd);
     wr(f, mc._xi.data(), C);
-    if (has_ds) wr(f, mc.doubleSideTransform.data(), 16);
+    if (has_ds) wr(f, my->doubleSideTransform.data(), 16);
     if (dsc)
         for (int c = 0; c < C; ++c) wr(f, dsc->camerasPose[c].data(), 16);
     const std::vector<float> x0 = mc.buildParas();
@@ -96,10 +106,10 @@ void dump_problem(MyMultiCameraCalibration& mc, const std::string& path) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string serials, data, config, ds, out = "multi-camera-results.xml", dump_p, dump_r;
+    std::string serials, data, config, ds, out = "multi-camera-results.xml", dump_p, dump_r, list;
     Size front(8, 11), back(7, 10);
-    bool single = false, init_only = false, double_side = false;
-    int device = 0, verbose = 0;
+    bool single = false, init_only = false, double_side = false, omni = false;
+    int device = 0, verbose = 0, ncams = 0, min_matches = 20;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto next = [&]() -> std::string {
@@ -120,12 +130,46 @@ int main(int argc, char** argv) {
         else if (a == "--dump-result") dump_r = next();
         else if (a == "--device") device = std::stoi(next());
         else if (a == "--verbose") verbose = 1;
+        else if (a == "--list") list = next();
+        else if (a == "--omni") omni = true;
+        else if (a == "--cameras") ncams = std::stoi(next());
+        else if (a == "--min-matches") min_matches = std::stoi(next());
         else {
             std::fprintf(stderr, "unknown argument %s\n", a.c_str());
             return 2;
         }
     }
     try {
+        if (!list.empty()) {   // the multi-camera tutorial's flow on the base class
+            if (ncams < 1) throw std::runtime_error("--list needs --cameras N");
+            MultiCameraCalibration multiCalib(omni ? MultiCameraCalibration::OMNIDIRECTIONAL
+                                                   : MultiCameraCalibration::PINHOLE,
+                                              ncams, list, 0.f, 0.f, verbose, 0, min_matches, 0,
+                                              TermCriteria(TermCriteria::COUNT, 20, 1e-7), device);
+            multiCalib.loadImages();
+            multiCalib.initialize();
+            if (!dump_p.empty()) dump_problem(multiCalib, dump_p);
+            if (init_only) {
+                std::printf("loaded: %zu edges, %zu vertices\n", multiCalib._edgeList.size(),
+                            multiCalib._vertexList.size());
+                return 0;
+            }
+            const double err = multiCalib.optimizeExtrinsics();
+            multiCalib.writeParameters(out);
+            if (!dump_r.empty()) {
+                std::ofstream r(dump_r);
+                char b[40];
+                std::snprintf(b, sizeof b, "%.17g", err);
+                r << "error_exact " << b << "\niterations " << multiCalib.iterations() << "\nx";
+                for (float v : multiCalib.buildParas()) {
+                    std::snprintf(b, sizeof b, " %.9g", v);
+                    r << b;
+                }
+                r << "\n";
+            }
+            std::printf("meanReprojectError %.9g after %d iterations\n", err, multiCalib.iterations());
+            return 0;
+        }
         const std::vector<std::string> cams = split(serials, ',');
         if (cams.empty() || data.empty() || config.empty()) {
             std::fprintf(stderr, "usage: %s --serials S0,S1,... --data DIR --config DIR [options]\n", argv[0]);

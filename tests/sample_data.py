@@ -130,3 +130,62 @@ def read_result(path):
         elif t[0] == "error_exact":
             out["error"] = float(t[1])
     return out
+
+
+def write_omni_list(p: "rig.Problem", root: str, ts0: int = 500, few_points=(), extra_views=0):
+    """An omnidirectional rig as the base MultiCameraCalibration reads it on this build
+    (include/mcc_multicalib.hpp loadImages): an imagelist_creator list `images.yaml` whose first
+    entry is the pattern and whose others are per-view corner files `cameraIdx-timestamp.yaml`
+    (imagePoints N x 1 2-channel, objectPoints N x 1 3-channel, imageSize), in the reference's
+    file naming (tutorials/multi_camera_tutorial.markdown).  few_points: edges written with only
+    15 points (dropped by nMiniMatches = 20).  extra_views: per camera, that many single-camera
+    views of wide-angle board poses (rig.make_omni_views with the camera's intrinsics) under
+    timestamps of their own -- what the per-camera intrinsic calibration needs beyond the rig's
+    distant shared views; they become one-edge photo vertices (the reference keeps those:
+    simplifyPhotoVertexs is commented out, src/multicalib.cpp:351).
+    Returns (list path, {file: edge (-1 - k for extra view k)}, photo timestamps)."""
+    os.makedirs(root, exist_ok=True)
+    stamps = ts0 + np.arange(p.n_photos)
+    files, names = {}, ["pattern.png"]
+    few = set(int(e) for e in few_points)
+    W, H = p.image_size
+    for e in range(p.n_edges):
+        c, ph = int(p.edge_cam[e]), int(p.edge_photo[e])
+        o, n = int(p.edge_off[e]), int(p.edge_n[e])
+        if e in few:
+            n = 15
+        name = f"{c}-{stamps[ph]}.yaml"
+        img = np.asarray(p.img[o:o + n], np.float64)
+        obj = np.asarray(p.obj[o:o + n], np.float64)
+        with open(os.path.join(root, name), "w") as f:
+            f.write("%YAML:1.0\n---\n")
+            f.write(f"imagePoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"2f\"\n   data: [ "
+                    + ", ".join(repr(float(v)) for v in img.ravel()) + " ]\n")
+            f.write(f"objectPoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"3f\"\n   data: [ "
+                    + ", ".join(repr(float(v)) for v in obj.ravel()) + " ]\n")
+            f.write(f"imageSize: [ {int(W)}, {int(H)} ]\n")
+        files[os.path.join(root, name)] = e
+        names.append(name)
+    k = 0
+    for c in range(p.n_cams):
+        if not extra_views:
+            break
+        v = rig.make_omni_views(extra_views, seed=100 + c, K=p.K[c], xi=float(p.xi[c]), D=p.D[c])
+        for i in range(v.n_views):
+            sl = slice(v.off[i], v.off[i + 1])
+            n = int(v.off[i + 1] - v.off[i])
+            name = f"{c}-{ts0 + p.n_photos + 1000 + k}.yaml"
+            with open(os.path.join(root, name), "w") as f:
+                f.write("%YAML:1.0\n---\n")
+                f.write(f"imagePoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"2f\"\n   data: [ "
+                        + ", ".join(repr(float(x)) for x in v.img[sl].ravel()) + " ]\n")
+                f.write(f"objectPoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"3f\"\n   data: [ "
+                        + ", ".join(repr(float(x)) for x in v.obj[sl].ravel()) + " ]\n")
+                f.write(f"imageSize: [ {int(W)}, {int(H)} ]\n")
+            files[os.path.join(root, name)] = -1 - k
+            names.append(name)
+            k += 1
+    lst = os.path.join(root, "images.yaml")
+    with open(lst, "w") as f:
+        f.write("%YAML:1.0\n---\nimages:\n" + "".join(f"   - {nm}\n" for nm in names))
+    return lst, files, stamps

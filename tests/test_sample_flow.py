@@ -261,3 +261,89 @@ def test_doubleside_two_pass_flow(sample, tmp_path):
     T = np.array(vals).reshape(4, 4)
     assert np.abs(T - _pose(xo[0])).max() <= 1e-3 * max(1.0, np.abs(T).max())
     assert np.abs(T[:3, 3] - p.x_true[3:6]).max() < 5.0   # near the synthetic truth
+
+
+# ---------------------------------------------------------------- base class, omnidirectional
+def _omni_rig():
+    return rig.make_config("config4", n_views=40, seed=21)
+
+
+EXTRA = 40
+
+
+def _camera_views(p, cam, few=()):
+    """One camera's views in the order the loader reads them (list order: the rig's edges, then
+    the extra single-camera views), minus the views with too few points; points as float32 (the
+    files hold the rig's float32 values)."""
+    few = set(int(e) for e in few)
+    es = [e for e in range(p.n_edges) if int(p.edge_cam[e]) == cam and e not in few]
+    objs = [p.obj[p.edge_off[e]:p.edge_off[e] + p.edge_n[e]] for e in es]
+    imgs = [p.img[p.edge_off[e]:p.edge_off[e] + p.edge_n[e]] for e in es]
+    v = rig.make_omni_views(EXTRA, seed=100 + cam, K=p.K[cam], xi=float(p.xi[cam]), D=p.D[cam])
+    for i in range(v.n_views):
+        objs.append(v.obj[v.off[i]:v.off[i + 1]])
+        imgs.append(v.img[v.off[i]:v.off[i + 1]])
+    offs = np.cumsum([0] + [len(o) for o in objs]).astype(np.int32)
+    obj = np.concatenate(objs).astype(np.float32).astype(np.float64)
+    img = np.concatenate(imgs).astype(np.float32).astype(np.float64)
+    return O.OmniViews(offs, obj, img), es
+
+
+def test_omni_list_reader_without_gpu(sample, tmp_path):
+    """The list / corner-file reader runs up to the first device call (the per-camera omnidir
+    calibration), which must fail loudly without a GPU."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("checks the no-GPU failure mode")
+    except Exception:
+        pass
+    p = _omni_rig()
+    lst, _, _ = SD.write_omni_list(p, str(tmp_path / "omni"))
+    r = subprocess.run([sample, "--list", lst, "--omni", "--cameras", str(p.n_cams), "--init-only"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "error" in r.stderr
+
+
+@pytest.mark.gpu
+def test_omni_base_class_flow(sample, tmp_path):
+    """MultiCameraCalibration(OMNIDIRECTIONAL, ...) over a corner-file list: per camera the GPU
+    omnidir calibration equals the oracle's on that camera's views; the problem loadImages +
+    initialize build has the rig's edges (views with <= nMiniMatches points dropped); the GPU
+    optimizeExtrinsics from the sample's own x0 equals the oracle run from it; the results file
+    carries xi_i."""
+    p = _omni_rig()
+    few = [3, 17]
+    lst, files, stamps = SD.write_omni_list(p, str(tmp_path / "omni"), few_points=few, extra_views=EXTRA)
+    dump, res, out = str(tmp_path / "p.bin"), str(tmp_path / "r.txt"), str(tmp_path / "res.xml")
+    _run(sample, ["--list", lst, "--omni", "--cameras", str(p.n_cams), "--min-matches", "20",
+                  "--dump-problem", dump, "--dump-result", res, "--out", out])
+    q, ts = SD.read_dump(dump)
+    assert q.model == rig.OMNI and q.n_cams == p.n_cams
+    assert q.n_edges <= p.n_edges - len(few) + EXTRA * p.n_cams
+    # intrinsics: exactly mcc_omnidir_calibrate of each camera's kept views in list order with the
+    # loader's TermCriteria(COUNT + EPS, 300, 1e-7) (its parity with the oracle restatement is
+    # tests/test_omnidir_calib.py's; the dense oracle would take minutes at ~70 views x 300 steps)
+    for c in range(p.n_cams):
+        v, _ = _camera_views(p, c, few)
+        rms, K, xi, D, om, t, idx, it = api.omnidir_calibrate(v.off, v.obj, v.img, p.image_size, 0, 3, 300, 1e-7)
+        assert rms < 0.5   # converged to the corner noise (0.2 px per axis)
+        np.testing.assert_array_equal(q.K[c], K.astype(np.float32))
+        assert q.xi[c] == np.float32(xi)
+        np.testing.assert_array_equal(q.D[c], D.astype(np.float32))
+    # the extrinsic optimisation from the sample's own x0 (TermCriteria(COUNT, 20, 1e-7))
+    r = SD.read_result(res)
+    xo, mo, ito, _ = O.Oracle(q).optimize(q.x0, crit_type=1, max_count=20, eps=1e-7)
+    assert r["iterations"] == ito == 20
+    assert abs(r["error"] - mo) <= 1e-6
+    # the dumped x is buildParas() after paras2vertex (pose -> Rodrigues): a rotation whose angle
+    # the update pushed past pi comes back as its equivalent (2 pi - angle about -axis), so the
+    # rotations are compared as matrices (near pi the float32 log round trip is good to ~1e-5:
+    # its axis error scales with 1 / sin(angle))
+    xg, xo6 = r["x"].reshape(-1, 6).astype(np.float64), xo.reshape(-1, 6).astype(np.float64)
+    for a, b in zip(xg, xo6):
+        assert np.abs(_rot(a[:3]) - _rot(b[:3])).max() <= 1e-4
+    assert np.abs(xg[:, 3:] - xo6[:, 3:]).max() <= 1e-5 * max(1.0, np.abs(xo6[:, 3:]).max())
+    root = ET.parse(out).getroot()
+    assert root.find("xi_0") is not None and root.find("nCameras").text.strip() == str(p.n_cams)
