@@ -123,9 +123,8 @@ struct mcc_problem {
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
-    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, W;
-    DevBuf<unsigned long long> contrib, gsum;   // fused step: LL words of the two reduction levels
-    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt_blk;
+    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
+    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
     DevBuf<int4> edge_info, items, pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
@@ -161,11 +160,6 @@ struct mcc_problem {
 };
 
 namespace {
-
-// k_linearize grid rows (diagnostic stamp rows): the photos, then the fused step's reducers
-size_t lin_rows(const mcc_problem* p) {
-    return (size_t)std::max(p->V, 1) + (p->fused ? (size_t)p->n_groups + 1 : 0);
-}
 
 mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
     return mcc::SolveCtx{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
@@ -217,9 +211,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.group_size = p->group_size; la.n_groups = p->n_groups;
     la.rank = p->rank; la.fuse_solve = rccl ? 0 : 1;
     la.peer = peer_ctx(p, peer && p->fused);
-    la.n_photos = p->V;
-    la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.packed = p->packed.p; la.W = p->W.p;
-    la.ll_timeout = 100000000;   // 1 s of s_memrealtime (100 MHz): a reducer waits ~1 photo workgroup at most
+    la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p; la.W = p->W.p;
     la.solve = solve_ctx(p, do_update);
     la.solve.stamps = nullptr;
     if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
@@ -255,7 +247,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     const bool split = rccl || peer || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
     sa.solve = solve_ctx(p, do_update);
-    sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * lin_rows(p) : nullptr;
+    sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
     if (rccl) {
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
@@ -355,7 +347,6 @@ int read_state(mcc_problem* p) {
 }
 
 int check_state_error(mcc_problem* p) {
-    if (p->h_state->error & 8) return fail(MCC_EHIP, "in-kernel reduction timed out (a photo workgroup did not deliver)");
     if (p->h_state->error & 4) return fail(MCC_ECOMM, "peer exchange timed out (a rank did not deliver)");
     if (p->h_state->error & 2) return fail(MCC_ENOTPD, "reduced camera system is not positive definite");
     if (p->h_state->error & 1) return fail(MCC_ENOTPD, "a photo normal-equation block is not positive definite");
@@ -575,12 +566,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->dg.alloc(p->m)); HIPC(p->delta.alloc(p->P));
     HIPC(p->photo_norm.alloc(2 * (size_t)V));
     if (p->fused) {
-        // LL words start at epoch 0, which no step uses (State::lepoch + 1 >= 1)
-        HIPC(p->contrib.alloc((size_t)2 * p->packed_len * std::max(V, 1)));
-        HIPC(hipMemset(p->contrib.p, 0, sizeof(unsigned long long) * p->contrib.n));
-        HIPC(p->gsum.alloc((size_t)2 * p->packed_len * p->n_groups));
-        HIPC(hipMemset(p->gsum.p, 0, sizeof(unsigned long long) * p->gsum.n));
+        HIPC(p->contrib.alloc((size_t)p->packed_len * std::max(V, 1)));
+        HIPC(p->gsum.alloc((size_t)p->packed_len * p->n_groups));
         HIPC(p->W.alloc((size_t)6 * p->m * std::max(V, 1)));
+        HIPC(p->cnt.alloc(p->n_groups + 1));
+        HIPC(hipMemset(p->cnt.p, 0, sizeof(int) * (p->n_groups + 1)));
     }
     HIPC(hipMemset(p->photo_norm.p, 0, sizeof(double) * 2 * std::max(V, 1)));
     HIPC(p->edge_sum.alloc(E));
@@ -616,7 +606,7 @@ void mcc_destroy(mcc_problem* p) {
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
-    p->contrib.release(); p->gsum.release(); p->W.release();
+    p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Hgp.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
@@ -761,7 +751,7 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     if (!p->stamps.p) {
-        const size_t n_st = mcc::kStampStride * lin_rows(p) + 8 * (size_t)(p->n_items + p->n_norm_chunks);
+        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + 8 * (size_t)(p->n_items + p->n_norm_chunks);
         HIPCHK(p->stamps.alloc(n_st));
         HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
         for (auto& g : p->gexec)

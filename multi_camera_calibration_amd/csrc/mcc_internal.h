@@ -19,11 +19,9 @@ struct State {
     double change;    // ||G|| / ||x|| of the last update
     double alpha;     // 0.95^(k+1) of the running step
     double cam_normG2, cam_normX2;   // global-block partials of the last update
-    int error;        // bit 0: photo block not PD, bit 1: camera system not PD, bit 2: peer timeout,
-                      // bit 3: in-kernel reduction timeout
+    int error;        // bit 0: photo block not PD, bit 1: camera system not PD, bit 2: peer timeout
     int pending;      // a solved photo update waits to be applied by the next k_linearize
     unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
-    unsigned int lepoch;  // fused steps completed (monotonic): the LL epoch of the in-kernel reduction
 };
 
 // Peer transport (multi-GPU without RCCL in the step): every rank's final arriver writes its packed
@@ -77,14 +75,13 @@ struct LinArgs {
     double* photo_norm;      // [2V] ||G||^2, ||x||^2 partials of the applied update
     long long* stamps;       // MCC_DIAG builds: [16V] s_memtime per phase
     // fused single-kernel step (m <= 30): every photo writes its packed contribution
-    // [S upper | r | jte_g | normG2 | normX2] as LL words; n_groups reducer workgroups (grid rows
-    // n_photos ..) each sum group_size consecutive photos in photo order as they land, and one
-    // final workgroup (the last grid row) sums the groups in order and solves (fuse_solve) or
-    // leaves the packed system for the all-reduce + k_solve
-    int fused, group_size, n_groups, rank, fuse_solve, n_photos;
-    unsigned long long* contrib;   // [V][2 Lc] LL words {epoch | one half of a double}
-    unsigned long long* gsum;      // [n_groups][2 Lc]
-    long long ll_timeout;          // s_memrealtime ticks a reducer waits before flagging error bit 3
+    // [S upper | r | jte_g | normG2 | normX2], a fixed-order two-level last-arriver reduction sums
+    // them (groups of group_size consecutive photos, then the groups), and the final arriver
+    // solves (fuse_solve) or leaves the packed system for the all-reduce + k_solve
+    int fused, group_size, n_groups, rank, fuse_solve;
+    double* contrib;         // [V * Lc]
+    double* gsum;            // [n_groups * Lc]
+    int* cnt;                // [n_groups + 1] tickets, zero between launches
     double* packed;          // [Lc]
     double* W;               // [V * 6m] per-photo pending-update matrix (next step's phase 0)
     SolveCtx solve;

@@ -9,9 +9,9 @@
 //                 27 normal-equation sums, chain rule to the photo / global blocks, 6x6 photo
 //                 inverse (register Gauss-Jordan), Schur factors Y'_e.
 //                 m <= 30 (single GPU): the WHOLE step is this one kernel -- per-photo packed
-//                 contributions as LL words, reducer rows after the photos (group sums in photo
-//                 order, then the final row: groups in order, stop test + reduced solve + camera
-//                 update; multi-GPU: with the in-kernel peer exchange of the packed system first).
+//                 contributions, a two-level write-through last-arriver reduction, and the final
+//                 arriver's stop test + reduced solve + camera update (multi-GPU: with the
+//                 in-kernel peer exchange of the packed system first).
 //   k_schur       m > 30 (or RCCL): camera-pair-block work items of S = sum H_gg - sum Y' H_gp^T
 //                 and r, plus norm chunks; two-level write-through hand-off into the packed system.
 //   k_solve       m > 30 / RCCL: [peer exchange], stop test, blocked Gauss-Jordan (16 x 16 blocks,
@@ -226,6 +226,8 @@ struct PhotoLds {
     double Hs[36], gs[6], Lm[36], z[6], il[6];
     double dgl[128];     // global-block delta of the previous solve (pending update)
     double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
+    double cn[2];        // state snapshot: camera-block ||G||^2, ||x||^2 of the last update
+    int iter0, pad1[3];  // state snapshot: completed updates
     int bn[8];           // per camera block: number of the photo's edges in it (fused step)
     unsigned char bl[5][64];   // per camera block: those edges in edge order
     // followed by the camera table [C][kCamStride], the intrinsics [C][kIntrStride] and the
@@ -786,64 +788,6 @@ __device__ __forceinline__ double sum_sc1(const double* p, int n, size_t stride)
     return v;
 }
 
-// ---------------------------------------------------------------- LL hand-off on one device
-// The fused step's reduction hands doubles over in the peer transport's LL form (below): a double
-// is two 8-B agent-scope relaxed stores (write-through, sc1) {epoch | low half}, {epoch | high
-// half}, and a reader polls until both words carry the step's epoch.  The writer needs no vmcnt
-// drain, no ticket and no fence.  The readers are dedicated reducer workgroups in the grid rows
-// after every photo: everything a reducer waits for was dispatched before it, so the scheme needs
-// no co-residency, and a reducer sums in photo / group order while the words land.
-__device__ __forceinline__ void ll_put(unsigned long long* w, double v, unsigned ep) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v), e = (unsigned long long)ep << 32;
-    __hip_atomic_store((gu64*)w, e | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu64*)(w + 1), e | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_sc1_u64(const unsigned long long* p) {
-    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// sum_{q < n} of the LL-encoded doubles at w + q * stride in q order.  A batch's loads are issued
-// together and every poll round re-issues all words still short of ep, so the batch completes one
-// round trip after its last word lands.  Gives up (timeout = true, value meaningless) once
-// s_memrealtime passes t0 + tmo.
-__device__ __forceinline__ double ll_sum(const unsigned long long* w, int n, size_t stride, unsigned ep, long long t0,
-                                         long long tmo, bool& timeout) {
-    constexpr int B = 24;
-    double v = 0.0;
-    for (int q0 = 0; q0 < n; q0 += B) {
-        unsigned long long lo[B], hi[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const unsigned long long* p = w + (size_t)min(q0 + u, n - 1) * stride;
-            lo[u] = ld_sc1_u64(p);
-            hi[u] = ld_sc1_u64(p + 1);
-        }
-        for (;;) {
-            bool all = true;
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                all &= q0 + u >= n || ((unsigned)(lo[u] >> 32) == ep && (unsigned)(hi[u] >> 32) == ep);
-            if (all || timeout) break;
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
-                timeout = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-            for (int u = 0; u < B; ++u) {
-                if (q0 + u < n && ((unsigned)(lo[u] >> 32) != ep || (unsigned)(hi[u] >> 32) != ep)) {
-                    const unsigned long long* p = w + (size_t)(q0 + u) * stride;
-                    lo[u] = ld_sc1_u64(p);
-                    hi[u] = ld_sc1_u64(p + 1);
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < B; ++u)
-            if (q0 + u < n) v += __longlong_as_double((long long)(((hi[u] & 0xffffffffull) << 32) | (lo[u] & 0xffffffffull)));
-    }
-    return v;
-}
-
 // ---------------------------------------------------------------- peer transport (PeerCtx)
 // System-scope relaxed 8-B stores / loads (global_store / global_load sc0 sc1): write-through to
 // the owner's memory over xGMI, reads from memory (the inbox is uncached besides).  No fence: an
@@ -921,114 +865,15 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2);
 
-// ---------------------------------------------------------------- fused step: reducer workgroups
-// Grid rows n_photos .. n_photos + n_groups - 1: group g sums the packed contributions of photos
-// [g G, g G + G) in photo order; the last row sums the n_groups group sums in group order into the
-// packed system, adds the stop-test norms, and runs the stop test, reduced solve and camera update
-// (fuse_solve) -- or, multi-GPU, the peer exchange first / only the packed system for RCCL.  The
-// same fixed-order two-level sum the photos' contributions always had (bitwise reproducible).
-__device__ __forceinline__ void fused_reduce(const LinArgs& a, double* smem) {
-    State* st = a.state;
-    const int tid = threadIdx.x;
-    if (st->done) return;
-    RSTAMP(14);
-    const unsigned ep = st->lepoch + 1u;   // this step's LL epoch (the final row bumps it)
-    const int m = a.global_dim, ntri = m * (m + 1) / 2, Lc = ntri + 2 * m + 2;
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    const int g = (int)blockIdx.x - a.n_photos;
-    bool timeout = false;
-    if (g < a.n_groups) {
-        const int G = a.group_size, g0 = g * G, gn = min(G, a.n_photos - g0);
-        for (int t = tid; t < Lc; t += blockDim.x) {
-            const double v = ll_sum(a.contrib + (size_t)g0 * 2 * Lc + 2 * t, gn, 2 * (size_t)Lc, ep, t0, a.ll_timeout,
-                                    timeout);
-            ll_put(a.gsum + (size_t)g * 2 * Lc + 2 * t, v, ep);
-        }
-        if (timeout) atomicOr(&st->error, 8);
-        RSTAMP(30);
-        RSTAMP(15);
-        return;
-    }
-    // ---- the final row: groups in order -> packed system [S upper | r | jte_g | normG2 | normX2]
-    double* S = smem;   // m*m + m doubles for the solve
-    double* rr = smem + m * m;
-    __shared__ double nrm2[2];
-    __shared__ int to_s;
-    const int iter0 = st->iter;
-    const double cnG = st->cam_normG2, cnX = st->cam_normX2;
-    if (tid == 0) to_s = 0;
-    __syncthreads();
-    auto place = [&](int t, double v) {
-        if (t < ntri) {
-            int i, j;
-            packed_ij(t, m, i, j);
-            S[i * m + j] = v;
-            S[j * m + i] = v;
-        } else if (t < ntri + m) {
-            rr[t - ntri] = v;
-        } else if (t >= ntri + 2 * m) {
-            nrm2[t - ntri - 2 * m] = v;
-        }
-    };
-    const bool peer = a.peer.nranks > 0;
-    for (int t = tid; t < Lc; t += blockDim.x) {
-        double v = ll_sum(a.gsum + 2 * t, a.n_groups, 2 * (size_t)Lc, ep, t0, a.ll_timeout, timeout);
-        if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
-            const int w = t - ntri - 2 * m;
-            if (iter0 > 0) {
-                if (a.rank == 0) v += w ? cnX : cnG;
-            } else {
-                v = 0.0;
-            }
-        }
-        if (!peer) place(t, v);
-        a.packed[t] = v;
-    }
-    if (timeout) to_s = 1;
-    RSTAMP(31);
-    STAMP(11);
-    __syncthreads();
-    // every photo and group row read st->lepoch before its words (which carry ep) were stored, so
-    // the bump cannot reach a reader of this step
-    if (tid == 0) {
-        st->lepoch = ep;
-        if (to_s) {
-            st->error |= 8;
-            st->done = 1;
-        }
-    }
-    if (to_s) { RSTAMP(15); return; }
-    if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
-        if (!peer_exchange(a.peer, st, a.packed)) { RSTAMP(15); return; }
-        for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);
-    }
-    if (!a.fuse_solve) { RSTAMP(15); return; }
-    __syncthreads();
-    STAMP(12);
-    SolveCtx sc = a.solve;
-#ifdef MCC_DIAG
-    sc.stamps = a.stamps ? a.stamps + kStampStride * (size_t)blockIdx.x + 20 : nullptr;   // slots 20..26
-#endif
-    solve_global<false>(sc, S, rr, nrm2[0], nrm2[1]);
-    STAMP(13);
-    RSTAMP(15);
-}
-
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
 template <int MODEL, bool RATIONAL, bool PRISM>
 __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    if (a.fused && (int)blockIdx.x >= a.n_photos) {   // the fused step's reducer rows
-        fused_reduce(a, smem);
-        return;
-    }
     const int photo = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // ---- round trip 1: everything indexed by the photo alone
     const int done = st->done, pending = st->pending;
-    const unsigned lep = st->lepoch + 1u;   // fused step: the LL epoch of this step's contribution
     const double alpha_prev = st->alpha;   // step factor of the pending update
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
@@ -1043,6 +888,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         a.stamps[kStampStride * (size_t)photo + 27] = ne;
     }
 #endif
+    extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
     PhotoLds& P = *reinterpret_cast<PhotoLds*>(smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double)));
     double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][kCamStride] = {R, Jl, T}
@@ -1060,6 +906,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     if (wave == 0) {
         if (lane < 6) xov = xg[lane];
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
+        else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
+        else if (lane == 10) P.iter0 = st->iter;
         if (pending && a.fused) {
             if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
@@ -1466,7 +1314,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     __syncthreads();
     STAMP(7);
     const int m = a.global_dim, ntri = m * (m + 1) / 2, Lc = ntri + 2 * m + 2;
-    unsigned long long* cv = a.contrib + (size_t)photo * 2 * Lc;
+    double* cv = a.contrib + (size_t)photo * Lc;
     for (int t = tid; t < Lc; t += blockDim.x) {
         double v = 0.0;
         if (t < ntri) {
@@ -1503,11 +1351,15 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         } else {
             v = P.nrm[t - ntri - 2 * m];
         }
-        ll_put(cv + 2 * t, v, lep);   // to the group's reducer row (fused_reduce)
+        st_sc1(cv + t, v);
     }
     STAMP(8);
     RSTAMP(29);
-    // the next step's pending-update matrix of this photo,
+    // ---- level 1: the last photo of a group sums the group in photo order
+    const int G = a.group_size, grp = photo / G, g0 = grp * G;
+    const int gn = min(G, (int)gridDim.x - g0);
+    const bool grp_last = arrive_last_sc1(a.cnt + grp, gn, a.stamps ? a.stamps + kStampStride * (size_t)photo + 28 : nullptr);
+    // the next step's pending-update matrix of this photo (after the ticket: off its drain),
     // W[k][6g + i] = sum over the photo's edges e of camera block g of Y'_e[i][k]
     for (int t = tid; t < 6 * m; t += blockDim.x) {
         const int k = t / m, col = t % m, g = col / 6, i = col % 6;
@@ -1515,6 +1367,68 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         for (int q = 0; q < P.bn[g]; ++q) w += el[P.bl[g][q]].Xg[i * 6 + k];
         a.W[(size_t)photo * 6 * m + t] = w;
     }
+    if (!grp_last) {
+        RSTAMP(15);
+        return;
+    }
+    STAMP(9);
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        v = sum_sc1(a.contrib + (size_t)g0 * Lc + t, gn, Lc);
+        st_sc1(a.gsum + (size_t)grp * Lc + t, v);
+    }
+    STAMP(10);
+    RSTAMP(30);
+    // ---- level 2: the last group sums the groups in order -> packed system
+    if (!arrive_last_sc1(a.cnt + a.n_groups, a.n_groups)) { RSTAMP(15); return; }
+    STAMP(11);
+    RSTAMP(31);
+    double* S = smem;            // the edge records are dead: m*m + m doubles for the solve
+    double* rr = smem + m * m;
+    __shared__ double nrm2[2];
+    const int iter0 = P.iter0;   // read before S overwrites the photo record
+    const double cnG = P.cn[0], cnX = P.cn[1];
+    __syncthreads();
+    auto place = [&](int t, double v) {
+        if (t < ntri) {
+            int i, j;
+            packed_ij(t, m, i, j);
+            S[i * m + j] = v;
+            S[j * m + i] = v;
+        } else if (t < ntri + m) {
+            rr[t - ntri] = v;
+        } else if (t >= ntri + 2 * m) {
+            nrm2[t - ntri - 2 * m] = v;
+        }
+    };
+    const bool peer = a.peer.nranks > 0;
+    for (int t = tid; t < Lc; t += blockDim.x) {
+        double v = 0.0;
+        v = sum_sc1(a.gsum + t, a.n_groups, Lc);
+        if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
+            const int w = t - ntri - 2 * m;
+            if (iter0 > 0) {
+                if (a.rank == 0) v += w ? cnX : cnG;
+            } else {
+                v = 0.0;
+            }
+        }
+        if (!peer) place(t, v);
+        a.packed[t] = v;
+    }
+    if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
+        if (!peer_exchange(a.peer, st, a.packed)) { RSTAMP(15); return; }
+        for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);
+    }
+    if (!a.fuse_solve) { RSTAMP(15); return; }
+    __syncthreads();
+    STAMP(12);
+    SolveCtx sc = a.solve;
+#ifdef MCC_DIAG
+    sc.stamps = a.stamps ? a.stamps + kStampStride * (size_t)photo + 20 : nullptr;   // slots 20..26
+#endif
+    solve_global<false>(sc, S, rr, nrm2[0], nrm2[1]);
+    STAMP(13);
     RSTAMP(15);
 }
 
@@ -2233,11 +2147,11 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 using namespace mcc;
 
 template <int MODEL>
-static hipError_t launch_lin_model(const LinArgs& a, int grid, size_t shmem, hipStream_t s, bool rational, bool prism) {
-    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), dim3(grid), dim3(256), shmem, s, a);
-    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), dim3(grid), dim3(256), shmem, s, a);
-    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), dim3(grid), dim3(256), shmem, s, a);
-    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), dim3(grid), dim3(256), shmem, s, a);
+static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
+    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), dim3(n_photos), dim3(256), shmem, s, a);
+    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), dim3(n_photos), dim3(256), shmem, s, a);
     return hipGetLastError();
 }
 
@@ -2256,13 +2170,10 @@ size_t mcc_solve_shmem(int m) {
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
     const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp);
-    if (a.fused && (a.n_photos != n_photos || a.n_groups < 1 || a.group_size * a.n_groups < n_photos))
-        return hipErrorInvalidValue;   // the reducer rows must cover every photo exactly once
-    const int grid = n_photos + (a.fused ? a.n_groups + 1 : 0);   // photos, then the fused step's reducers
     switch (model) {
-        case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, grid, shmem, s, false, false);
-        case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, grid, shmem, s, rational, prism);
-        default: return launch_lin_model<MCC_MODEL_PINHOLE>(a, grid, shmem, s, rational, prism);
+        case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
+        case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
+        default: return launch_lin_model<MCC_MODEL_PINHOLE>(a, n_photos, shmem, s, rational, prism);
     }
 }
 

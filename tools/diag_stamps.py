@@ -5,15 +5,12 @@ run time: read its shares.
 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_stamps.py [config] [views]
 
-Slots per photo row (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written;
-14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit, 29 contribution written; 16, 18, 19
-phase-0 detail (loads, back-solve, photo Rodrigues).  Fused step: after the photo rows come the
-reducer rows (n_groups group rows: 14 start, 30 group sum written, 15 exit; then the final row:
-14 start, 31 / 11 every group sum received, 12 system placed, 13 solved, 20..26 solve detail).
-s_memtime is per XCD, so only differences within one workgroup are meaningful; the cross-workgroup
-timeline uses the s_memrealtime slots.
+Slots per workgroup (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written,
+9 group ticket won, 10 group sum written, 11 final ticket won, 12 system assembled, 13 solved
+(fused step); 14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit; 16, 18, 19 phase-0 detail
+(loads, back-solve, photo Rodrigues).  s_memtime is per XCD,
+so only differences within one workgroup are meaningful; the cross-workgroup timeline uses 14/15.
 """
-import math
 import os
 import sys
 
@@ -42,12 +39,8 @@ def main():
     ba.synchronize()
     raw = ba.stamps().reshape(-1)
     nv = max(p.n_photos, 1)
-    fused = ba.m <= 30
-    gs = max(1, math.ceil(math.sqrt(nv)))
-    nred = (nv + gs - 1) // gs + 1 if fused else 0   # group rows + the final row
     s = raw[:32 * nv].reshape(nv, 32).astype(np.float64)
-    red = raw[32 * nv:32 * (nv + nred)].reshape(nred, 32).astype(np.float64)
-    sch = raw[32 * (nv + nred):].reshape(-1, 8).astype(np.float64)
+    sch = raw[32 * nv:].reshape(-1, 8).astype(np.float64)
     s = s[s[:, 0] > 0]
     d = np.diff(s[:, :8], axis=1)
     print(f"{cfg}: {len(s)} workgroups stamped (s_memtime ticks)")
@@ -56,14 +49,20 @@ def main():
     print(f"  {'linearize total':16s} {med(s[:, 7] - s[:, 0])}")
     print(f"  phase 0: loads+partials {med(s[:, 16] - s[:, 0])}; back-solve/update {med(s[:, 18] - s[:, 16])}; "
           f"photo Rodrigues {med(s[:, 19] - s[:, 18])}; barrier {med(s[:, 1] - s[:, 19])}")
-    fused = fused and (s[:, 8] > 0).any()
+    fused = (s[:, 8] > 0).any()
     if fused:
         print(f"  {'contribution':16s} {med(s[:, 8] - s[:, 7])}")
-        F = red[-1]
-        print(f"  final row: system placed {F[12] - F[11]:.0f}, solve {F[13] - F[12]:.0f}")
-        sv = F[20:27]
-        print(f"  solve: stop test (wave 0) {sv[4] - sv[0]:.0f} incl. barrier; GJ (wave 1) {sv[2] - sv[1]:.0f}; "
-              f"after GJ -> update start {sv[5] - sv[4]:.0f}; update {sv[6] - sv[5]:.0f}; tail {F[13] - sv[6]:.0f}")
+        g = s[s[:, 9] > 0]
+        print(f"  group reducers: {len(g)}; ticket {med(g[:, 9] - g[:, 8])} (drain+barrier {med(g[:, 28] - g[:, 8])}); "
+              f"group sum {med(g[:, 10] - g[:, 9])}")
+        print(f"  all photos: contribution drain+barrier {med(s[:, 28] - s[:, 8])}")
+        f = s[s[:, 11] > 0]
+        if len(f):
+            F = f[0]
+            print(f"  final: ticket {F[11] - F[10]:.0f}, assemble {F[12] - F[11]:.0f}, solve {F[13] - F[12]:.0f}")
+            sv = F[20:27]
+            print(f"  solve: stop test (wave 0) {sv[4] - sv[0]:.0f} incl. barrier; GJ (wave 1) {sv[2] - sv[1]:.0f}; "
+                  f"after GJ -> update start {sv[5] - sv[4]:.0f}; update {sv[6] - sv[5]:.0f}; tail {F[13] - sv[6]:.0f}")
     r0, r1 = s[:, 14], s[:, 15]
     ok = r1 > 0
     if ok.any():
@@ -72,17 +71,13 @@ def main():
               f"exit median {(np.median(r1[ok]) - t0) / 100:.2f}; last exit {(r1[ok].max() - t0) / 100:.2f}")
         print(f"  workgroup residency (us): {med((r1[ok] - r0[ok]) / 100)}")
         c = s[:, 29]
-        if fused and (c > 0).any():
+        if (c > 0).any():
             cc = c[c > 0]
-            G = red[:-1]
-            F = red[-1]
-            us = lambda v: (v - t0) / 100   # noqa: E731
-            print(f"  contributions written (us): first {us(cc.min()):.2f} median {us(np.median(cc)):.2f} "
-                  f"last {us(cc.max()):.2f}")
-            print(f"  group rows: start first {us(G[:, 14].min()):.2f} last {us(G[:, 14].max()):.2f}; "
-                  f"sum written median {us(np.median(G[:, 30])):.2f} last {us(G[:, 30].max()):.2f}; "
-                  f"lag after the group's last photo: {med((G[:, 30] - np.array([c[k * gs:(k + 1) * gs].max() for k in range(len(G))])) / 100)} us")
-            print(f"  final row: start {us(F[14]):.2f}; all group sums {us(F[31]):.2f}; end {us(F[15]):.2f}")
+            g = s[s[:, 30] > 0][:, 30]
+            f = s[s[:, 31] > 0][:, 31]
+            print(f"  contributions written (us): first {(cc.min() - t0) / 100:.2f} median {(np.median(cc) - t0) / 100:.2f} "
+                  f"last {(cc.max() - t0) / 100:.2f}; group sums done: last {(g.max() - t0) / 100:.2f}; "
+                  f"final ticket won {(f.max() - t0) / 100:.2f}; end {(r1[ok].max() - t0) / 100:.2f}")
     # placement / edge count vs linearisation time (slot 25: xcc << 32 | HW_ID, slot 27: edges)
     hw = s[:, 25].astype(np.int64)
     if (hw != 0).any():
