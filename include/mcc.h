@@ -63,7 +63,9 @@ typedef struct mcc_problem mcc_problem;
  * identity and is not optimised), photo vertices n_cams.. are given as photo indices
  * 0..n_photos-1.  Edges are in reference order (_edgeList).  Parameters follow buildParas
  * (src/multicalib.cpp:422-440): [cam1..cam(C-1), photo0..] x (rvec, tvec), or for DOUBLESIDE
- * (src/doubleSide.cpp:233-261): [ds, photo0..]. */
+ * (src/doubleSide.cpp:233-261): [ds, photo0..].  n_photos >= 1 and n_edges >= 1 (MCC_EINVAL
+ * otherwise: the reference's mean error is 0/0 without observations); at most 22 cameras
+ * (global block m <= 128, the reduced solve's LDS-resident matrix) and 1024 corners per edge. */
 typedef struct mcc_desc {
     int model;
     int n_cams, n_photos, n_edges;

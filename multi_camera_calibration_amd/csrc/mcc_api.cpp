@@ -373,6 +373,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     *out = nullptr;
     if (d->model < 0 || d->model > 2) return fail(MCC_EINVAL, "unknown model");
     if (d->n_cams < 1 || d->n_photos < 0 || d->n_edges < 0) return fail(MCC_EINVAL, "bad sizes");
+    // the reference's meanReProjError is 0 / 0 without observations (src/multicalib.cpp:989), and
+    // a photo vertex exists only through an edge (getPhotoVertex, :323-346); a rank of a sharded
+    // problem needs photos of its own to take part in the per-step exchange
+    if (d->n_photos < 1 || d->n_edges < 1) return fail(MCC_EINVAL, "no photo vertices / observations");
     if (d->model != MCC_MODEL_DOUBLESIDE && d->n_cams < 2) return fail(MCC_EINVAL, "need >= 2 cameras");
     if (d->model == MCC_MODEL_OMNI && (d->nd != 4 || !d->xi)) return fail(MCC_EINVAL, "omni needs nd == 4 and xi");
     if (d->model != MCC_MODEL_OMNI && !(d->nd == 4 || d->nd == 5 || d->nd == 8 || d->nd == 12 || d->nd == 14))

@@ -7,6 +7,7 @@ RCCL runtimes but makes no device call until mcc_create).
 * without a GPU, creating a problem fails loudly (MCC_EHIP) -- the product has no CPU fallback.
 """
 import ctypes
+import dataclasses
 import os
 import re
 import subprocess
@@ -56,11 +57,16 @@ def test_null_arguments_rejected(L):
     assert L.mcc_partition_photos(3, 0, None, None, 0, None) == MCC_EINVAL
 
 
-@pytest.mark.parametrize("bad", ["model", "nd", "edge_range", "omni_back", "too_many_corners"])
+@pytest.mark.parametrize("bad", ["model", "nd", "edge_range", "omni_back", "too_many_corners", "empty"])
 def test_invalid_problem_rejected_before_device_work(bad):
     p = rig.make_config("config1")
     kw = {}
-    if bad == "model":
+    if bad == "empty":   # no photos / edges: the reference's mean error would be 0/0
+        p = dataclasses.replace(p, n_photos=0, edge_cam=p.edge_cam[:0], edge_photo=p.edge_photo[:0],
+                                edge_side=p.edge_side[:0], edge_off=p.edge_off[:0], edge_n=p.edge_n[:0],
+                                obj=p.obj[:0], img=p.img[:0], x0=p.x0[:6 * (p.n_cams - 1)],
+                                x_true=p.x_true[:6 * (p.n_cams - 1)], timestamps=p.timestamps[:0])
+    elif bad == "model":
         kw["model"] = 7
     elif bad == "nd":
         p.D = np.zeros((p.n_cams, 6), np.float32)
