@@ -97,6 +97,16 @@ def main():
             sel = share == k
             print(f"  {int(k)} workgroup(s) on the CU: {sel.sum()} photos, linearize {med(lin[sel])}")
         print(f"  distinct CUs {len(cnt)}, xcc histogram {np.bincount(xcc.astype(int), minlength=8).tolist()}")
+        # co-resident pairs: is wave 0 (the serial phases' wave) of both on the same SIMD?
+        simd = (hw & 0xFFFFFFFF) >> 4 & 0x3
+        same, diff = [], []
+        for k in np.unique(key):
+            idx = np.nonzero(key == k)[0]
+            if len(idx) == 2:
+                (same if simd[idx[0]] == simd[idx[1]] else diff).extend(lin[idx].tolist())
+        print(f"  CU pairs with wave 0 on the same SIMD: {len(same) // 2}, linearize {med(np.array(same))}; "
+              f"different SIMDs: {len(diff) // 2}, linearize {med(np.array(diff))}")
+        print(f"  wave-0 SIMD histogram {np.bincount(simd.astype(int), minlength=4).tolist()}")
     ok = sch[:, 0] > 0
     if ok.any():
         it = sch[ok]
