@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -57,6 +58,34 @@ struct DevBuf {
         p = nullptr;
     }
 };
+
+// Idle non-blocking streams per device, kept for the next problem: hipStreamDestroy costs ~2 ms
+// (most of an mcc_destroy) and creating one more than that.  A stream is returned only after it
+// has drained and its graphs and events are gone.
+struct StreamPool {
+    std::mutex mu;
+    std::vector<std::pair<int, hipStream_t>> idle;   // (device, stream)
+    hipError_t take(int device, hipStream_t* s) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (size_t i = 0; i < idle.size(); ++i)
+                if (idle[i].first == device) {
+                    *s = idle[i].second;
+                    idle.erase(idle.begin() + (long)i);
+                    return hipSuccess;
+                }
+        }
+        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    void give(int device, hipStream_t s) {
+        std::lock_guard<std::mutex> lk(mu);
+        idle.emplace_back(device, s);
+    }
+};
+StreamPool& stream_pool() {
+    static StreamPool* pool = new StreamPool();   // never destroyed: streams outlive static teardown
+    return *pool;
+}
 
 // Host restatement of cvRodrigues2 matrix -> vector (with the polar re-orthonormalisation)
 // used once per problem for fixed transforms (doubleSideTransform2vec,
@@ -410,7 +439,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             return bail(fail(MCC_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e))); \
     } while (0)
     HIPC(hipSetDevice(d->device));
-    HIPC(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    HIPC(stream_pool().take(d->device, &p->stream));
     if (const char* g = std::getenv("MCC_GRAPH")) p->use_graph = std::atoi(g) != 0;
 
     // distortion specialisation (zero coefficients are exact no-ops in OpenCV's formula)
@@ -596,7 +625,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
 void mcc_destroy(mcc_problem* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
-    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    const bool drained = p->stream && hipStreamSynchronize(p->stream) == hipSuccess;
     for (auto& g : p->gexec)
         if (g) (void)hipGraphExecDestroy(g);
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
@@ -618,7 +647,8 @@ void mcc_destroy(mcc_problem* p) {
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
-    if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused
+    else if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
 
