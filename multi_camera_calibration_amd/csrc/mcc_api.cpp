@@ -137,7 +137,7 @@ struct mcc_problem {
     long long corners = 0;
     bool rational = false, prism = false;
     int has_back = 0;
-    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
+    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0, max_ppp = 0;
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
@@ -152,9 +152,9 @@ struct mcc_problem {
     // device buffers
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
-    DevBuf<double> ds_rt, Y, Hgg, Hgp, gg, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
-    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
-    DevBuf<int4> edge_info, items, pairs;
+    DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
+    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk, photo_pair_ptr;
+    DevBuf<int4> edge_info, items, photo_pairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
     int packed_len = 0, ntri = 0;
@@ -224,7 +224,9 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.cam_rt = p->cam_rt.p; la.ds_rt = p->ds_rt.p;
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
-    la.Y = p->Y.p; la.Hgg = p->Hgg.p; la.Hgp = p->Hgp.p; la.gg = p->gg.p; la.zp = p->zp.p;
+    la.Y = p->Y.p; la.zp = p->zp.p;
+    la.photo_pair_ptr = p->photo_pair_ptr.p; la.photo_pairs = p->photo_pairs.p; la.pairprod = p->pairprod.p;
+    la.max_ppp = p->fused ? 0 : p->max_ppp;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
     la.gblock = p->edge_gblock.p;
@@ -262,8 +264,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
 
     SchurArgs sa{};
     sa.state = p->state.p;
-    sa.items = p->items.p; sa.pairs = p->pairs.p;
-    sa.Y = p->Y.p; sa.Hgg = p->Hgg.p; sa.Hgp = p->Hgp.p; sa.gg = p->gg.p; sa.gp_tot = p->gp_tot.p;
+    sa.items = p->items.p;
+    sa.pairprod = p->pairprod.p;
     sa.item_out = p->item_out.p;
     sa.n_items = p->n_items;
     sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
@@ -499,21 +501,30 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     const int nb = p->m / 6;
     p->nblk = nb * (nb + 1) / 2;
     auto blk_index = [nb](int b1, int b2) { return b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1); };
-    std::vector<std::vector<int4>> blk_pairs(p->nblk);
-    for (int v = 0; v < V; ++v)
+    // photo-major: {local e1, local e2, self, block-major slot}; k_linearize writes each pair's
+    // product at its slot, k_schur sums a block's slots in order
+    std::vector<int4> photo_pairs;
+    std::vector<int> photo_pair_ptr(V + 1, 0);
+    std::vector<std::vector<int>> blk_src(p->nblk);   // photo-major index of each block's pairs
+    for (int v = 0; v < V; ++v) {
         for (int e1 = photo_ptr[v]; e1 < photo_ptr[v + 1]; ++e1) {
             if (gblock[e1] < 0) continue;
             for (int e2 = photo_ptr[v]; e2 < photo_ptr[v + 1]; ++e2) {
                 if (gblock[e2] < 0 || gblock[e1] > gblock[e2]) continue;
-                blk_pairs[blk_index(gblock[e1], gblock[e2])].push_back(make_int4(e1, e2, v, e1 == e2 ? 1 : 0));
+                blk_src[blk_index(gblock[e1], gblock[e2])].push_back((int)photo_pairs.size());
+                photo_pairs.push_back(make_int4(e1 - photo_ptr[v], e2 - photo_ptr[v], e1 == e2 ? 1 : 0, -1));
             }
         }
-    std::vector<int4> pairs, items;
+        photo_pair_ptr[v + 1] = (int)photo_pairs.size();
+        p->max_ppp = std::max(p->max_ppp, photo_pair_ptr[v + 1] - photo_pair_ptr[v]);
+    }
+    std::vector<int4> items;
     std::vector<int> block_items(p->nblk + 1, 0);
+    int n_slots = 0;
     for (int b = 0; b < p->nblk; ++b) {
-        const int begin = (int)pairs.size();
-        pairs.insert(pairs.end(), blk_pairs[b].begin(), blk_pairs[b].end());
-        const int end = (int)pairs.size();
+        const int begin = n_slots;
+        for (int src : blk_src[b]) photo_pairs[src].w = n_slots++;
+        const int end = n_slots;
         // <= 24 work items per block keeps the last-arriver assembly short; >= 20 pairs per item
         // (4 per sub-chunk thread) keeps the item workgroups busy
         const int per_item = std::max(20, (end - begin + 23) / 24);
@@ -524,10 +535,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         block_items[b + 1] = (int)items.size();
     }
     for (int b1 = 0; b1 < nb; ++b1)
-        if (blk_pairs[blk_index(b1, b1)].empty())
+        if (blk_src[blk_index(b1, b1)].empty())
             return bail(fail(MCC_EINVAL, "global block " + std::to_string(b1) + " has no observations"));
     p->n_items = (int)items.size();
-    p->n_pairs = (int)pairs.size();
+    p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
     // small camera blocks: one kernel per Gauss-Newton step (MCC_FUSED=0 forces the k_schur path)
@@ -578,12 +589,13 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->cam_pose.upload(cp.data(), 16 * C));
     HIPC(p->ds_rt.upload(ds_rt, 6));
     HIPC(p->alpha.upload(alpha.data(), alpha.size()));
-    HIPC(p->pairs.upload(pairs.data(), pairs.size()));
+    HIPC(p->photo_pairs.upload(photo_pairs.data(), photo_pairs.size()));
+    HIPC(p->photo_pair_ptr.upload(photo_pair_ptr.data(), V + 1));
     HIPC(p->items.upload(items.data(), items.size()));
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
-    HIPC(p->Y.alloc(36 * (size_t)E)); HIPC(p->Hgg.alloc(36 * (size_t)E)); HIPC(p->gg.alloc(6 * (size_t)E));
-    HIPC(p->Hgp.alloc(36 * (size_t)E));
+    HIPC(p->Y.alloc(36 * (size_t)E));
+    HIPC(p->pairprod.alloc(48 * (size_t)(p->fused ? 0 : p->n_pairs)));
     HIPC(p->zp.alloc(6 * (size_t)V));
     HIPC(p->gp_tot.alloc(6 * (size_t)V));
     // + 24 zeroed items of padding: the assembly loads a fixed 24 items per block unconditionally
@@ -613,9 +625,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
-    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused, p->max_cpp) > 160 * 1024)
+    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused, p->max_cpp, p->max_ppp) > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many edges / corners per photo for the LDS staging"));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused, p->max_cpp));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused, p->max_cpp, p->max_ppp));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -640,11 +652,12 @@ void mcc_destroy(mcc_problem* p) {
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
-    p->ds_rt.release(); p->Y.release(); p->Hgg.release(); p->gg.release(); p->Hgp.release(); p->zp.release();
+    p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
-    p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->pairs.release();
+    p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->photo_pairs.release();
+    p->photo_pair_ptr.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused

@@ -63,9 +63,11 @@ struct LinArgs {
     int nd, global_dim, n_cams, has_back;
     // outputs
     double* Y;        // [36E] Schur factors Y'_e = Hgp_e Hpp^-1
-    double* Hgg;      // [36E] (k_schur path)
-    double* Hgp;      // [36E] (k_schur path)
-    double* gg;       // [6E] (k_schur path)
+    // k_schur path: the photo's Schur pair products, [48] per pair at its block-major slot
+    const int* photo_pair_ptr;   // [V+1] photo-major ranges of photo_pairs
+    const int4* photo_pairs;     // {local e1, local e2, self, slot}
+    double* pairprod;            // [48 * pairs] {S_ab entries (36), r_a (6), JTE_a (6)}
+    int max_ppp;                 // most pairs of one photo (LDS staging)
     double* zp;       // [6V] z' = Hpp^-1 gp
     double* gp_tot;   // [6V] photo JTE
     float* resid;     // optional [2*corners] float32 residuals (debug)
@@ -91,8 +93,7 @@ struct LinArgs {
 struct SchurArgs {
     State* state;
     const int4* items;   // {block, pair_begin, pair_end, -}
-    const int4* pairs;   // {e1, e2, photo, self}
-    const double* Y; const double* Hgg; const double* Hgp; const double* gg; const double* gp_tot;
+    const double* pairprod;   // [48 * pairs] per-pair products written by k_linearize, block-major
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;
     const double* photo_norm; int n_photos;
@@ -139,9 +140,9 @@ struct ErrArgs {
 }  // namespace mcc
 
 // launch wrappers (mcc_kernels.hip)
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp);
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp, int max_ppp);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);

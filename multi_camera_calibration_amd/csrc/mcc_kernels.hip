@@ -877,6 +877,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     const double alpha_prev = st->alpha;   // step factor of the pending update
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
+    const int pp0 = a.fused ? 0 : a.photo_pair_ptr[photo];
+    const int npp = a.fused ? 0 : a.photo_pair_ptr[photo + 1] - pp0;
     if (done) return;
     STAMP(0);
     RSTAMP(14);
@@ -894,6 +896,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][kCamStride] = {R, Jl, T}
     double* ktab = ctab + kCamStride * a.n_cams;         // [C][kIntrStride] intrinsics
     float* cs = reinterpret_cast<float*>(ktab + kIntrStride * a.n_cams);   // [5][max_cpp] corners
+    int4* ppl = reinterpret_cast<int4*>(reinterpret_cast<char*>(cs) + ((5 * sizeof(float) * a.max_cpp + 15) & ~(size_t)15));
     const int c0 = a.photo_corner[photo];
     const int ncs = a.photo_corner[photo + 1] - c0;
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
@@ -1012,6 +1015,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             EdgeLds& L = el[le];
             L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
         }
+        // k_schur path: the photo's Schur pairs (local edges, self, block-major slot)
+        for (int q = tid - 128; q < npp; q += 128) ppl[q] = a.photo_pairs[pp0 + q];
         // the photo's corners are contiguous (photo-major layout): stage all five streams
         for (int q = tid - 128; q < ncs; q += 128) {
             const size_t c = (size_t)c0 + q;
@@ -1279,16 +1284,37 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) y += L.Hgp[i * 6 + k] * Hi[k * 6 + j];
         }
-        if (a.fused) {   // (W below replaces the edge-indexed Y' of the split path)
-            L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the contribution below
-        } else {
-            a.Y[36 * e + ij] = y;
-            a.Hgg[36 * e + ij] = L.has_global ? L.Hgg[ij] : 0.0;
-            a.Hgp[36 * e + ij] = L.has_global ? L.Hgp[ij] : 0.0;
-            if (j == 0) a.gg[6 * e + i] = L.has_global ? L.gg[i] : 0.0;
-        }
+        L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the products below
+        if (!a.fused) a.Y[36 * e + ij] = y;   // (fused: W below replaces the edge-indexed Y')
     }
     if (!a.fused) {
+        // k_schur path: the photo's Schur pair products, each at its block-major slot, so k_schur
+        // streams and sums them in slot order:  S_ab entries ([self] Hgg_a - Y'_a Hgp_b^T),
+        // r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
+        // thread (pair k, row i): row i of the 6x6 product and entry i of r and JTE
+        __syncthreads();
+        for (int t = tid; t < 6 * npp; t += blockDim.x) {
+            const int k = t / 6, i = t % 6;
+            const int4 pp = ppl[k];   // {local e1, local e2, self, slot}
+            const EdgeLds& La = el[pp.x];
+            const EdgeLds& Lb = el[pp.y];
+            double y[6];
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk) y[kk] = La.Xg[i * 6 + kk];
+            double* out = a.pairprod + 48 * (size_t)pp.w;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double d = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * Lb.Hgp[j * 6 + kk];
+                out[i * 6 + j] = pp.z ? La.Hgg[i * 6 + j] - d : -d;
+            }
+            double d = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk) d += y[kk] * gs[kk];
+            out[36 + i] = pp.z ? La.gg[i] - d : 0.0;
+            out[42 + i] = pp.z ? La.gg[i] : 0.0;
+        }
 #ifdef MCC_DIAG
         __syncthreads();
         STAMP(7);
@@ -1766,8 +1792,10 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 }
 
 // ---------------------------------------------------------------- k_schur
-// Work item: pairs [begin, end) of one camera-pair block (S_ab -= Y'_a Hgp_b^T, r_a += gg_a - Y'_a gp).  Thread t < 240: entry q = t % 48
-// (0..35: S entry, 36..41: r entry, 42..47: JTE of the global block), sub-chunk s = t / 48.
+// Work item: slots [begin, end) of one camera-pair block.  k_linearize wrote each pair's product
+// at its slot (48 doubles: [self] Hgg_a - Y'_a Hgp_b^T, [self] (gg_a - Y'_a gp), [self] gg_a), so an
+// item streams and sums them.  Thread t < 240: entry q = t % 48 (0..35: S entry, 36..41: r entry,
+// 42..47: JTE of the global block), sub-chunk s = t / 48.
 // Norm items sum 256 photos' norm partials.  Hand-off in two write-through levels (sc1 stores,
 // tickets, no fences): the last item of each camera-pair block sums the block's items in item
 // order into the packed system [S upper (m(m+1)/2) | r (m) | jte_g (m) | normG2 | normX2]; the
@@ -1788,32 +1816,18 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         const int q = tid % 48, sub = tid / 48;
         double s = 0.0;
         if (sub < kSub) {
-#pragma unroll 4
-            for (int p = it.y + sub; p < it.z; p += kSub) {
-                const int4 pr = a.pairs[p];   // {e1, e2, photo, self}
-                const double* Y1 = a.Y + 36 * (size_t)pr.x;
-                if (q < 36) {
-                    const int i = q / 6, j = q % 6;
-                    const double* H2 = a.Hgp + 36 * (size_t)pr.y;
-                    double t = 0.0;
+            // the products k_linearize wrote at the block's slots: independent coalesced loads,
+            // eight in flight per thread
+            const double* pp = a.pairprod + q;
+            int p = it.y + sub;
+            for (; p + 7 * kSub < it.z; p += 8 * kSub) {
+                double v[8];
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * H2[j * 6 + k];
-                    s -= t;
-                    if (pr.w) s += a.Hgg[36 * (size_t)pr.x + q];
-                } else if (pr.w) {
-                    const int i = (q - 36) % 6;
-                    const double gi = a.gg[6 * (size_t)pr.x + i];
-                    if (q < 42) {
-                        const double* gpt = a.gp_tot + 6 * (size_t)pr.z;
-                        double t = 0.0;
+                for (int u = 0; u < 8; ++u) v[u] = pp[48 * (size_t)(p + u * kSub)];
 #pragma unroll
-                        for (int k = 0; k < 6; ++k) t += Y1[i * 6 + k] * gpt[k];
-                        s += gi - t;
-                    } else {
-                        s += gi;
-                    }
-                }
+                for (int u = 0; u < 8; ++u) s += v[u];
             }
+            for (; p < it.z; p += kSub) s += pp[48 * (size_t)p];
             part[sub][q] = s;
         }
         __syncthreads();
@@ -2155,10 +2169,11 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     return hipGetLastError();
 }
 
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp) {
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
                        (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
-                       ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15);
+                       ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15) +
+                       (fused ? 0 : sizeof(int4) * (size_t)max_ppp);
     return fused ? std::max(lin, (size_t)(m * m + m) * sizeof(double)) : lin;
 }
 
@@ -2169,7 +2184,7 @@ size_t mcc_solve_shmem(int m) {
 }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp);
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp, a.max_ppp);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
         case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
@@ -2177,9 +2192,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp) {
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp, int max_ppp) {
     hipError_t err = hipSuccess;
-    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused, max_cpp);
+    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused, max_cpp, max_ppp);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
         for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
