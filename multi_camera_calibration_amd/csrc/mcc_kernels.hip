@@ -1615,29 +1615,27 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
         else { const int u = t - ncol; i = u / pad; j = m + u % pad; }   // rows < m, columns m..M-1
         A[i * ld + j] = i == j ? 1.0 : 0.0;
     }
-    // the packed upper triangle row by row (row i is contiguous from packed_index(i, i)): wave w
-    // takes rows w, w + 4, ..., twelve rows' loads in flight per lane; (i, j) and (j, i) written
-    constexpr int RB = 12;
-    for (int i0 = wave; i0 < m; i0 += RB * nw) {
-        double v[RB][2];
+    // the packed upper triangle, flat: thread t takes entries t, t + 256, ... (sixteen loads in
+    // flight, one memory round trip up to m = 90), row i from the quadratic's root with a one-step
+    // fix-up; (i, j) and (j, i) written
+    const int nt = m * (m + 1) / 2;
+    constexpr int PB = 16;
+    for (int t0 = tid; t0 < nt; t0 += PB * (int)blockDim.x) {
+        double v[PB];
 #pragma unroll
-        for (int q = 0; q < RB; ++q) {
-            const int i = min(i0 + q * nw, m - 1), base = packed_index(i, i, m), len = m - i;
+        for (int u = 0; u < PB; ++u) v[u] = packed[min(t0 + u * (int)blockDim.x, nt - 1)];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) v[q][h] = packed[base + min(lane + 64 * h, len - 1)];
-        }
-#pragma unroll
-        for (int q = 0; q < RB; ++q) {
-            const int i = i0 + q * nw;
-            if (i >= m) continue;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int j = i + lane + 64 * h;
-                if (j < m) {
-                    A[i * ld + j] = v[q][h];
-                    A[j * ld + i] = v[q][h];
-                }
-            }
+        for (int u = 0; u < PB; ++u) {
+            const int t = t0 + u * (int)blockDim.x;
+            if (t >= nt) break;
+            const double b = 2.0 * m + 1.0;
+            int i = (int)((b - sqrt(b * b - 8.0 * t)) * 0.5);
+            i = max(0, min(i, m - 1));
+            if (packed_index(i, i, m) > t) --i;
+            else if (i + 1 < m && packed_index(i + 1, i + 1, m) <= t) ++i;
+            const int j = i + (t - packed_index(i, i, m));
+            A[i * ld + j] = v[u];
+            A[j * ld + i] = v[u];
         }
     }
     if (tid < M) x[tid] = xr;
