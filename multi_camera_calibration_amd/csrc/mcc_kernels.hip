@@ -867,7 +867,9 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
-template <int MODEL, bool RATIONAL, bool PRISM>
+// FUSED: the m <= 30 single-kernel step (a.fused); !FUSED: the k_schur path's linearisation.  Two
+// instantiations, so neither carries the other's code.
+template <int MODEL, bool RATIONAL, bool PRISM, bool FUSED>
 __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
     const int photo = blockIdx.x;
@@ -877,8 +879,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     const double alpha_prev = st->alpha;   // step factor of the pending update
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
-    const int pp0 = a.fused ? 0 : a.photo_pair_ptr[photo];
-    const int npp = a.fused ? 0 : a.photo_pair_ptr[photo + 1] - pp0;
+    const int pp0 = FUSED ? 0 : a.photo_pair_ptr[photo];
+    const int npp = FUSED ? 0 : a.photo_pair_ptr[photo + 1] - pp0;
     if (done) return;
     STAMP(0);
     RSTAMP(14);
@@ -911,7 +913,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
         else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
         else if (lane == 10) P.iter0 = st->iter;
-        if (pending && a.fused) {
+        if (FUSED && pending) {
             if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
             // W (written by the previous step) is indexed by the photo alone, so every operand
@@ -1016,7 +1018,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
         }
         // k_schur path: the photo's Schur pairs (local edges, self, block-major slot)
-        for (int q = tid - 128; q < npp; q += 128) ppl[q] = a.photo_pairs[pp0 + q];
+        if (!FUSED)
+            for (int q = tid - 128; q < npp; q += 128) ppl[q] = a.photo_pairs[pp0 + q];
         // the photo's corners are contiguous (photo-major layout): stage all five streams
         for (int q = tid - 128; q < ncs; q += 128) {
             const size_t c = (size_t)c0 + q;
@@ -1029,7 +1032,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     }
     STAMP(16);
     if (wave == 0) {
-        if (pending && a.fused) {
+        if (FUSED && pending) {
             // fused back-substitution of the previous step: dp_k = z'_k - sum_c part(k, c),
             // the ten partials of component k summed in c order through LDS by lane k
             if (lane < 60) P.dgl[lane] = part;
@@ -1078,7 +1081,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         STAMP(18);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
-            if (pending && a.fused) {   // norms of the applied update (independent of the Rodrigues chain)
+            if (FUSED && pending) {   // norms of the applied update (independent of the Rodrigues chain)
                 double g2 = 0.0, x2 = 0.0;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) {
@@ -1285,9 +1288,9 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             for (int k = 0; k < 6; ++k) y += L.Hgp[i * 6 + k] * Hi[k * 6 + j];
         }
         L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the products below
-        if (!a.fused) a.Y[36 * e + ij] = y;   // (fused: W below replaces the edge-indexed Y')
+        if (!FUSED) a.Y[36 * e + ij] = y;   // (fused: W below replaces the edge-indexed Y')
     }
-    if (!a.fused) {
+    if (!FUSED) {
         // k_schur path: the photo's Schur pair products, each at its block-major slot, so k_schur
         // streams and sums them in slot order:  S_ab entries ([self] Hgg_a - Y'_a Hgp_b^T),
         // r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
@@ -2158,12 +2161,17 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 // ---------------------------------------------------------------- launch wrappers
 using namespace mcc;
 
+template <int MODEL, bool FUSED>
+static void launch_lin_variant(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
+    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
+    else hipLaunchKernelGGL((k_linearize<MODEL, false, false, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
+}
 template <int MODEL>
 static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
-    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), dim3(n_photos), dim3(256), shmem, s, a);
-    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), dim3(n_photos), dim3(256), shmem, s, a);
+    if (a.fused) launch_lin_variant<MODEL, true>(a, n_photos, shmem, s, rational, prism);
+    else launch_lin_variant<MODEL, false>(a, n_photos, shmem, s, rational, prism);   // (MCC_FUSED=0 too)
     return hipGetLastError();
 }
 
@@ -2194,9 +2202,13 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int m
     hipError_t err = hipSuccess;
     const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused, max_cpp, max_ppp);
     if (shmem > 64 * 1024) {
-#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
-        for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
-                             SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true), SETA(2, true, true)})
+#define SETA(M, R, P, F) hipFuncSetAttribute((const void*)&k_linearize<M, R, P, F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
+        for (hipError_t e : {SETA(0, false, false, true), SETA(0, true, false, true), SETA(0, false, true, true),
+                             SETA(0, true, true, true), SETA(1, false, false, true), SETA(2, false, false, true),
+                             SETA(2, true, false, true), SETA(2, false, true, true), SETA(2, true, true, true),
+                             SETA(0, false, false, false), SETA(0, true, false, false), SETA(0, false, true, false),
+                             SETA(0, true, true, false), SETA(1, false, false, false), SETA(2, false, false, false),
+                             SETA(2, true, false, false), SETA(2, false, true, false), SETA(2, true, true, false)})
             if (e != hipSuccess) err = e;
 #undef SETA
     }
