@@ -1611,36 +1611,42 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
     const int nb = (m + 15) / 16, M = 16 * nb, ld = M + 1, ntri = m * (m + 1) / 2;
     // rhs, padding and the packed triangle: every global load is issued before the first LDS store
     const double xr = tid < m ? packed[ntri + tid] : 0.0;   // M <= 128 <= blockDim.x
-    for (int t = tid; t < M * M - m * m; t += blockDim.x) {   // padding: rows / columns m .. M-1
-        const int pad = M - m, ncol = pad * M;                 // t < ncol: rows m..M-1 (all columns)
-        int i, j;
-        if (t < ncol) { i = m + t / M; j = t % M; }
-        else { const int u = t - ncol; i = u / pad; j = m + u % pad; }   // rows < m, columns m..M-1
-        A[i * ld + j] = i == j ? 1.0 : 0.0;
-    }
-    // the packed upper triangle, flat: thread t takes entries t, t + 256, ... (sixteen loads in
-    // flight, one memory round trip up to m = 90), row i from the quadratic's root with a one-step
-    // fix-up; (i, j) and (j, i) written
+    // the packed upper triangle: thread t takes the sixteen contiguous entries 16t .. 16t+15
+    // (eight 16-B loads in flight, one memory round trip up to m = 90); the row of the first from
+    // the quadratic's root with a one-step fix-up, the rest by stepping along the row; (i, j) and
+    // (j, i) written
     const int nt = m * (m + 1) / 2;
     constexpr int PB = 16;
-    for (int t0 = tid; t0 < nt; t0 += PB * (int)blockDim.x) {
+    for (int t0 = PB * tid; t0 < nt; t0 += PB * (int)blockDim.x) {
         double v[PB];
+        if (t0 + PB <= nt) {
+            const double2* p2 = reinterpret_cast<const double2*>(packed + t0);   // t0 even: 16-B aligned
 #pragma unroll
-        for (int u = 0; u < PB; ++u) v[u] = packed[min(t0 + u * (int)blockDim.x, nt - 1)];
+            for (int u = 0; u < PB / 2; ++u) { const double2 w = p2[u]; v[2 * u] = w.x; v[2 * u + 1] = w.y; }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PB; ++u) v[u] = packed[min(t0 + u, nt - 1)];
+        }
+        const double b = 2.0 * m + 1.0;
+        int i = (int)((b - sqrt(b * b - 8.0 * t0)) * 0.5);
+        i = max(0, min(i, m - 1));
+        if (packed_index(i, i, m) > t0) --i;
+        else if (i + 1 < m && packed_index(i + 1, i + 1, m) <= t0) ++i;
+        int j = i + (t0 - packed_index(i, i, m));
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
-            const int t = t0 + u * (int)blockDim.x;
-            if (t >= nt) break;
-            const double b = 2.0 * m + 1.0;
-            int i = (int)((b - sqrt(b * b - 8.0 * t)) * 0.5);
-            i = max(0, min(i, m - 1));
-            if (packed_index(i, i, m) > t) --i;
-            else if (i + 1 < m && packed_index(i + 1, i + 1, m) <= t) ++i;
-            const int j = i + (t - packed_index(i, i, m));
-            A[i * ld + j] = v[u];
-            A[j * ld + i] = v[u];
+            if (t0 + u < nt) {
+                A[i * ld + j] = v[u];
+                A[j * ld + i] = v[u];
+            }
+            if (++j == m) { ++i; j = i; }
         }
     }
+    // padding: rows m .. M-1 (every column) and columns m .. M-1 of rows < m
+    for (int i = m + wave; i < M; i += nw)
+        for (int j = lane; j < M; j += 64) A[i * ld + j] = i == j ? 1.0 : 0.0;
+    for (int i = tid; i < m; i += blockDim.x)
+        for (int j = m; j < M; ++j) A[i * ld + j] = 0.0;
     if (tid < M) x[tid] = xr;
     __syncthreads();
     GJB_STAMP(0);
