@@ -138,6 +138,7 @@ struct mcc_problem {
     bool rational = false, prism = false;
     int has_back = 0;
     int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0, max_ppp = 0;
+    size_t n_pair_doubles = 0;   // Schur pair-product slots (36 or 48 doubles each)
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
@@ -512,7 +513,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             for (int e2 = photo_ptr[v]; e2 < photo_ptr[v + 1]; ++e2) {
                 if (gblock[e2] < 0 || gblock[e1] > gblock[e2]) continue;
                 blk_src[blk_index(gblock[e1], gblock[e2])].push_back((int)photo_pairs.size());
-                photo_pairs.push_back(make_int4(e1 - photo_ptr[v], e2 - photo_ptr[v], e1 == e2 ? 1 : 0, -1));
+                photo_pairs.push_back(make_int4(e1 - photo_ptr[v], e2 - photo_ptr[v],
+                                                (e1 == e2 ? 1 : 0) | (gblock[e1] == gblock[e2] ? 2 : 0), -1));
             }
         }
         photo_pair_ptr[v + 1] = (int)photo_pairs.size();
@@ -520,20 +522,35 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     }
     std::vector<int4> items;
     std::vector<int> block_items(p->nblk + 1, 0);
+    // slot sizes: 48 doubles on a diagonal camera-pair block (S entries, r, JTE), 36 off the
+    // diagonal (no self pair there, so r and JTE would be zeros); pair .w = the slot's offset in
+    // doubles; item = {block, first slot's offset, slots, slot size}
     int n_slots = 0;
+    size_t n_doubles = 0;
     for (int b = 0; b < p->nblk; ++b) {
+        int b1 = 0;
+        while (b1 + 1 < nb && blk_index(b1 + 1, b1 + 1) <= b) ++b1;
+        const int stride = blk_index(b1, b1) == b ? 48 : 36;
         const int begin = n_slots;
-        for (int src : blk_src[b]) photo_pairs[src].w = n_slots++;
+        const size_t base = n_doubles;
+        for (int src : blk_src[b]) {
+            photo_pairs[src].w = (int)n_doubles;
+            n_doubles += stride;
+            ++n_slots;
+        }
+        if (n_doubles > (size_t)INT32_MAX) return bail(fail(MCC_EINVAL, "too many Schur pairs"));
         const int end = n_slots;
         // <= 24 work items per block keeps the last-arriver assembly short; >= 20 pairs per item
         // (4 per sub-chunk thread) keeps the item workgroups busy
         const int per_item = std::max(20, (end - begin + 23) / 24);
-        for (int s = begin; s < end; s += per_item) items.push_back(make_int4(b, s, std::min(end, s + per_item), 0));
+        for (int s = begin; s < end; s += per_item)
+            items.push_back(make_int4(b, (int)(base + (size_t)(s - begin) * stride), std::min(end, s + per_item) - s, stride));
         // a block no photo couples gets one empty item: its last arriver writes the block's zeros
         // (every packed entry is rewritten each step; the all-reduce leaves sums there)
-        if (begin == end) items.push_back(make_int4(b, begin, end, 0));
+        if (begin == end) items.push_back(make_int4(b, (int)base, 0, stride));
         block_items[b + 1] = (int)items.size();
     }
+    p->n_pair_doubles = n_doubles;
     for (int b1 = 0; b1 < nb; ++b1)
         if (blk_src[blk_index(b1, b1)].empty())
             return bail(fail(MCC_EINVAL, "global block " + std::to_string(b1) + " has no observations"));
@@ -595,7 +612,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E));
-    HIPC(p->pairprod.alloc(48 * (size_t)(p->fused ? 0 : p->n_pairs)));
+    HIPC(p->pairprod.alloc(p->fused ? 0 : p->n_pair_doubles));
     HIPC(p->zp.alloc(6 * (size_t)V));
     HIPC(p->gp_tot.alloc(6 * (size_t)V));
     // + 24 zeroed items of padding: the assembly loads a fixed 24 items per block unconditionally

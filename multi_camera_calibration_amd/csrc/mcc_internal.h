@@ -65,8 +65,8 @@ struct LinArgs {
     double* Y;        // [36E] Schur factors Y'_e = Hgp_e Hpp^-1
     // k_schur path: the photo's Schur pair products, [48] per pair at its block-major slot
     const int* photo_pair_ptr;   // [V+1] photo-major ranges of photo_pairs
-    const int4* photo_pairs;     // {local e1, local e2, self, slot}
-    double* pairprod;            // [48 * pairs] {S_ab entries (36), r_a (6), JTE_a (6)}
+    const int4* photo_pairs;     // {local e1, local e2, self | diagonal block << 1, slot offset (doubles)}
+    double* pairprod;            // per pair {S_ab entries (36), [diagonal block] r_a (6), JTE_a (6)}
     int max_ppp;                 // most pairs of one photo (LDS staging)
     double* zp;       // [6V] z' = Hpp^-1 gp
     double* gp_tot;   // [6V] photo JTE
@@ -93,7 +93,7 @@ struct LinArgs {
 struct SchurArgs {
     State* state;
     const int4* items;   // {block, pair_begin, pair_end, -}
-    const double* pairprod;   // [48 * pairs] per-pair products written by k_linearize, block-major
+    const double* pairprod;   // 48 (diagonal block) or 36 doubles per pair, written by k_linearize, block-major
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;
     const double* photo_norm; int n_photos;

@@ -1304,19 +1304,22 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             double y[6];
 #pragma unroll
             for (int kk = 0; kk < 6; ++kk) y[kk] = La.Xg[i * 6 + kk];
-            double* out = a.pairprod + 48 * (size_t)pp.w;
+            double* out = a.pairprod + (size_t)pp.w;   // 48-double slot on a diagonal block, else 36
+            const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
                 double d = 0.0;
 #pragma unroll
                 for (int kk = 0; kk < 6; ++kk) d += y[kk] * Lb.Hgp[j * 6 + kk];
-                out[i * 6 + j] = pp.z ? La.Hgg[i * 6 + j] - d : -d;
+                out[i * 6 + j] = self ? La.Hgg[i * 6 + j] - d : -d;
             }
-            double d = 0.0;
+            if (diag) {
+                double d = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < 6; ++kk) d += y[kk] * gs[kk];
-            out[36 + i] = pp.z ? La.gg[i] - d : 0.0;
-            out[42 + i] = pp.z ? La.gg[i] : 0.0;
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * gs[kk];
+                out[36 + i] = self ? La.gg[i] - d : 0.0;
+                out[42 + i] = self ? La.gg[i] : 0.0;
+            }
         }
 #ifdef MCC_DIAG
         __syncthreads();
@@ -1800,7 +1803,8 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 
 // ---------------------------------------------------------------- k_schur
 // Work item: slots [begin, end) of one camera-pair block.  k_linearize wrote each pair's product
-// at its slot (48 doubles: [self] Hgg_a - Y'_a Hgp_b^T, [self] (gg_a - Y'_a gp), [self] gg_a), so an
+// at its slot (48 doubles: [self] Hgg_a - Y'_a Hgp_b^T, [self] (gg_a - Y'_a gp), [self] gg_a; 36 on an
+// off-diagonal block, which has no self pair), so an
 // item streams and sums them.  Thread t < 240: entry q = t % 48 (0..35: S entry, 36..41: r entry,
 // 42..47: JTE of the global block), sub-chunk s = t / 48.
 // Norm items sum 256 photos' norm partials.  Hand-off in two write-through levels (sc1 stores,
@@ -1819,22 +1823,24 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     __shared__ double part[kSub][48];
     __shared__ double red[256];
     if (item < a.n_items) {
-        const int4 it = a.items[item];   // {block, begin, end, -}
-        const int q = tid % 48, sub = tid / 48;
+        const int4 it = a.items[item];   // {block, first slot's offset (doubles), slots, slot size 48 | 36}
+        const int q = tid % 48, sub = tid / 48, sz = it.w;
         double s = 0.0;
         if (sub < kSub) {
             // the products k_linearize wrote at the block's slots: independent coalesced loads,
-            // eight in flight per thread
-            const double* pp = a.pairprod + q;
-            int p = it.y + sub;
-            for (; p + 7 * kSub < it.z; p += 8 * kSub) {
-                double v[8];
+            // eight in flight per thread (entries >= 36 of an off-diagonal block: none, zeros)
+            if (q < sz) {
+                const double* pp = a.pairprod + (size_t)it.y + q;
+                int p = sub;
+                for (; p + 7 * kSub < it.z; p += 8 * kSub) {
+                    double v[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = pp[48 * (size_t)(p + u * kSub)];
+                    for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)sz * (p + u * kSub)];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) s += v[u];
+                    for (int u = 0; u < 8; ++u) s += v[u];
+                }
+                for (; p < it.z; p += kSub) s += pp[(size_t)sz * p];
             }
-            for (; p < it.z; p += kSub) s += pp[48 * (size_t)p];
             part[sub][q] = s;
         }
         __syncthreads();
