@@ -6,13 +6,26 @@
 One "step" = one pass of the hot path over the whole problem: linearisation of every corner
 (residual + Jacobian), normal-equation reduction, Schur solve, float32 update
 (MultiCameraCalibration::optimizeExtrinsics loop body, src/multicalib.cpp:481-506).
-Workload: BASELINE.json configs[1] (4 pinhole cameras, 500 synthetic 11x8-board views) per
-rank; N > 1 ranks (one process per GPU, launched by torch.distributed.run) weak-scale it: the rig
-has 500*N views, photo vertices are sharded and each step exchanges the reduced camera system
+
+Headline workload: BASELINE.json configs[1] (4 pinhole cameras, 500 synthetic 11x8-board views)
+per rank.  N > 1 ranks (one process per GPU, launched by torch.distributed.run) weak-scale it: the
+rig has 500*N views, photo vertices are sharded and each step exchanges the reduced camera system
 once: over the peer transport (mcc_peer_*: the final arriving workgroup of each rank writes its
 system into every peer's inbox over xGMI and solves, one kernel per step) when the handshake
-passes on every rank, else with one RCCL all-reduce (MCC_TRANSPORT=rccl forces it).  Rank 0 prints
-one JSON line.
+passes on every rank, else with one RCCL all-reduce (MCC_TRANSPORT=rccl forces it).
+
+Timing: an untimed clock ramp (>= --ramp-seconds of steps, the same step count on every rank),
+W warmup steps, then exactly K steps between barriers (max over ranks); the dominant kernel is
+then timed with HIP events over a window of max(100, K) further launches.
+
+Extra keys (same JSON line):
+  * N = 1: "configs" -- configs 3, 4 and 5 of BASELINE.json at full size on this GPU (ms per
+    step, corner evals/s, k_linearize time and HBM-roofline fraction);
+  * N > 1: "strong" -- the BASELINE multi-GPU rigs at their fixed size split over the N ranks
+    (config3: 16 cameras x 5k views; config5: 8-camera double-sided board x 2k views), the
+    strong-scaling curve north_star names;
+  * "cpu_baseline" (the OpenMP Schur port on the same workload) and "cpu_baseline_ref_faithful"
+    (the reference's own algorithm -- dense J, J^T J, Jacobi-CG x2 -- single-threaded on config1).
 
 MCC_BENCH_SAME_DEVICE=1 puts every rank on device 0 with the peer transport only (RCCL refuses
 two ranks on one device): a rehearsal of the N > 1 code path on a one-GPU box, not a scaling
@@ -22,6 +35,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -34,14 +48,18 @@ sys.path.insert(0, ROOT)
 from multi_camera_calibration_amd import api, rig  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_PEAK_TFS = 78.6    # MI355X FP64 vector peak, AMD spec
 METRIC = "corner residual+Jacobian evals/sec + ms/LM-iter; RMS reproj-err vs ref"
 
 
-def rendezvous_id(rank: int, world: int) -> bytes:
-    """Share the RCCL unique id among the ranks of one node (torchrun's agent is every rank's
-    parent, so its pid names the launch)."""
-    port = os.environ.get("MASTER_PORT", "0")
-    path = f"/tmp/mcc_ncclid_{os.getppid()}_{port}"
+def _launch_key() -> str:
+    return f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+
+
+def rendezvous_id(rank: int, tag: str) -> bytes:
+    """Share an RCCL unique id among the ranks of one node (torchrun's agent is every rank's
+    parent, so its pid names the launch; tag names the problem)."""
+    path = f"/tmp/mcc_ncclid_{_launch_key()}_{tag}"
     if rank == 0:
         uid = api.unique_id()
         tmp = path + ".tmp"
@@ -61,12 +79,12 @@ def rendezvous_id(rank: int, world: int) -> bytes:
         time.sleep(0.05)
 
 
-def setup_transport(ba, rank: int, world: int, same_device: bool) -> str:
+def setup_transport(ba, rank: int, world: int, same_device: bool, tag: str) -> str:
     """RCCL communicator (distinct devices) plus, unless MCC_TRANSPORT=rccl, the peer transport;
     all ranks agree on the transport over RCCL before it is used."""
-    key = f"/tmp/mcc_peer_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+    key = f"/tmp/mcc_peer_{_launch_key()}_{tag}"
     if not same_device:
-        ba.comm_init(rendezvous_id(rank, world), world, rank)
+        ba.comm_init(rendezvous_id(rank, tag), world, rank)
     if os.environ.get("MCC_TRANSPORT", "peer") == "rccl":
         if same_device:
             raise SystemExit("MCC_BENCH_SAME_DEVICE needs the peer transport")
@@ -91,9 +109,6 @@ def setup_transport(ba, rank: int, world: int, same_device: bool) -> str:
     return "rccl"
 
 
-FP64_PEAK_TFS = 78.6   # MI355X FP64 vector peak, AMD spec
-
-
 def load_profile(prefix: str, config: str, n_views: int):
     """The committed rocprofv3 --pmc result for this workload (profiles/<prefix>_*.json)."""
     best = None
@@ -111,22 +126,98 @@ def load_profile(prefix: str, config: str, n_views: int):
     return best
 
 
-def load_traffic(config: str, n_views: int):
-    """Per-launch HBM bytes of k_linearize from the committed rocprofv3 --pmc pass, if one
-    exists for this workload (profiles/traffic_*.json, written by tools/pmc_traffic.py)."""
-    best = None
-    pdir = os.path.join(ROOT, "profiles")
-    if not os.path.isdir(pdir):
-        return None
-    for fn in sorted(os.listdir(pdir)):
-        if fn.startswith("traffic_") and fn.endswith(".json"):
-            try:
-                d = json.load(open(os.path.join(pdir, fn)))
-            except Exception:
-                continue
-            if d.get("config") == config and d.get("n_views") == n_views:
-                best = d
-    return best
+def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
+    """Clock ramp (same step count on every rank: each step may exchange with the peers),
+    W warmup steps, K timed steps between barriers (max over ranks), then the HIP-event window
+    of the dominant kernel over `window` launches."""
+    ba.step(8)
+    ba.synchronize()
+    t0 = time.perf_counter()
+    ba.step(16)
+    ba.synchronize()
+    per = ba.allreduce_max((time.perf_counter() - t0) / 16)
+    n_ramp = int(min(200000, max(64, math.ceil(ramp_s / max(per, 1e-7)))))
+    t0 = time.perf_counter()
+    ba.step(n_ramp)
+    ba.synchronize()
+    ramp_wall = time.perf_counter() - t0
+    ba.step(warmup)
+    ba.synchronize()
+    ba.barrier()
+    t0 = time.perf_counter()
+    ba.step(steps)
+    ba.synchronize()
+    ba.barrier()
+    t1 = time.perf_counter()
+    dt = ba.allreduce_max(t1 - t0)
+    ba.timing_begin()
+    ba.step(window)
+    lin_ms, step_ms_ev, nlaunch = ba.timing_end()
+    lin_ms = ba.allreduce_max(lin_ms)
+    step_ms_ev = ba.allreduce_max(step_ms_ev)
+    return dict(dt=dt, lin_ms=lin_ms, step_ms_ev=step_ms_ev, nlaunch=nlaunch,
+                ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)})
+
+
+def roofline(st, lin_ms, tr=None):
+    achieved = st["alg_bytes"] / (lin_ms * 1e-3) / 1e9
+    return {
+        "bound": "hbm",
+        "kernel": "k_linearize",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": (tr["bytes_per_launch"] if tr else None),
+        "alg_bytes_per_launch": st["alg_bytes"],
+        "alg_bytes_formula": "20 B/corner (float32 obj xyz + img uv) + 280 B/edge (SURVEY.md 8(d))",
+        "kernel_ms_per_launch": lin_ms,
+    }
+
+
+def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
+    """One BASELINE config at full size on this GPU (N = 1 extra key)."""
+    t0 = time.time()
+    p = rig.make_config(name)
+    gen_s = time.time() - t0
+    ba = api.BundleAdjuster(p, device=device)
+    try:
+        ba.set_params(p.x0)
+        m = measure(ba, steps, warmup, 0.15, max(100, steps))
+        st = ba.stats()
+    finally:
+        ba.close()
+    ms = m["dt"] / steps * 1e3
+    out = {"cameras": p.n_cams, "views": p.n_photos, "edges": p.n_edges, "corners_per_step": p.n_corners,
+           "model": {rig.PINHOLE: "pinhole", rig.OMNI: "omnidir", rig.DOUBLESIDE: "doubleside"}[p.model],
+           "steps": steps, "ms_per_step": ms, "corner_evals_per_s": p.n_corners / (ms * 1e-3),
+           "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
+           "roofline": roofline(st, m["lin_ms"]), "rig_generation_s": round(gen_s, 2)}
+    fp = load_profile("fp64", name, p.n_photos)
+    if fp and fp.get("fp64_flops_per_launch"):
+        tf = fp["fp64_flops_per_launch"] / (m["lin_ms"] * 1e-3) / 1e12
+        out["fp64_valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFS,
+                            "flops_per_corner": fp["fp64_flops_per_corner"]}
+    return out
+
+
+def strong_line(name: str, rank: int, world: int, local_rank: int, same_device: bool, steps: int = 100):
+    """A BASELINE multi-GPU rig at its fixed size, photo vertices split over the ranks."""
+    full = rig.make_config(name)
+    owner = api.partition_photos(full, world)
+    prob = rig.subset_photos(full, np.nonzero(owner == rank)[0])
+    ba = api.BundleAdjuster(prob, device=0 if same_device else local_rank)
+    try:
+        transport = setup_transport(ba, rank, world, same_device, f"strong_{name}")
+        ba.set_params(prob.x0)
+        m = measure(ba, steps, 10, 0.15, max(100, steps))
+    finally:
+        ba.close()
+    ms = m["dt"] / steps * 1e3
+    return {"views": full.n_photos, "cameras": full.n_cams, "corners_per_step": full.n_corners,
+            "value": full.n_corners / (ms * 1e-3), "unit": "corner evals/s", "ms_per_step": ms,
+            "n_gpus": world, "transport": transport, "kernel_ms_per_launch": m["lin_ms"],
+            "step_ms_events": m["step_ms_ev"], "scaling": "strong"}
 
 
 def cpu_baseline(prob, target_s: float):
@@ -150,6 +241,27 @@ def cpu_baseline(prob, target_s: float):
                 ms_per_step=dt / n * 1e3)
 
 
+def cpu_baseline_ref_faithful():
+    """The reference's own algorithm on one host core (SURVEY.md 8(d)(1) 'ref-faithful'): per
+    Gauss-Newton step a zero-filled dense J (2 sum N x P), JTJ = J^T J and JTE = J^T E as dense
+    products, Eigen-style Jacobi CG solved twice (src/mymulticalib.cpp:680-805,
+    src/multicalib.cpp:565-592); the whole optimizeExtrinsics run on config1."""
+    from oracle import oracle_py as O
+    p = rig.make_config("config1")
+    o = O.Oracle(p)
+    t0 = time.perf_counter()
+    _, mean, it, _ = o.optimize(p.x0, crit_type=3, max_count=200, eps=1e-7, solver="dense_j")
+    dt = time.perf_counter() - t0
+    rows = 2 * p.n_corners
+    c2 = rig.CONFIGS["config2"]
+    return dict(value=p.n_corners * it / dt, unit="corner evals/s", cores=1, kind="port",
+                ms_per_step=dt / it * 1e3, iterations=it, meanReProjError=mean,
+                sample=f"config1 (2 cameras, 20 views, 9x6 board): the whole optimizeExtrinsics, {it} steps of dense "
+                       f"J ({rows} x {p.n_params}) + J^T J + Jacobi-CG x2, single thread, {dt:.3f} s wall",
+                config2="skipped: its dense J is 345k x 3018 doubles (8.3 GB) and J^T J alone is ~1.6e12 "
+                        "multiply-adds per step (tens of minutes on one core), beyond a bench run")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,9 +269,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="config2")
     ap.add_argument("--views", type=int, default=None, help="views per rank (default: the config's)")
+    ap.add_argument("--ramp-seconds", type=float, default=0.25, help="untimed clock ramp before the warmup")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the per-config / strong-scaling extra keys")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,36 +292,27 @@ def main():
     else:
         prob = full
     ba = api.BundleAdjuster(prob, device=0 if same_device else local_rank)
-    transport = setup_transport(ba, rank, world, same_device) if world > 1 else "none"
+    transport = setup_transport(ba, rank, world, same_device, "weak") if world > 1 else "none"
     ba.set_params(prob.x0)
 
-    # ---- warmup, then exactly K timed steps between barriers
-    ba.step(args.warmup)
-    ba.synchronize()
-    ba.barrier()
-    t0 = time.perf_counter()
-    ba.step(args.steps)
-    ba.synchronize()
-    ba.barrier()
-    t1 = time.perf_counter()
-    dt = ba.allreduce_max(t1 - t0)
-
-    # ---- dominant kernel (k_linearize) duration with HIP events on the problem's stream
-    ba.timing_begin()
-    ba.step(min(256, max(8, args.steps // 4)))
-    lin_ms, step_ms_ev, nlaunch = ba.timing_end()
-    lin_ms = ba.allreduce_max(lin_ms)
+    m = measure(ba, args.steps, args.warmup, args.ramp_seconds, max(100, args.steps))
     st = ba.stats()
-    corners_local = st["corners"]
     corners_total = float(full.n_corners)
-    value = corners_total * args.steps / dt
-    ms_per_step = dt / args.steps * 1e3
+    value = corners_total * args.steps / m["dt"]
+    ms_per_step = m["dt"] / args.steps * 1e3
+    ba.close()
+
+    strong = {}
+    if world > 1 and not args.no_extra:
+        for name in ("config3", "config5"):
+            strong[name] = strong_line(name, rank, world, local_rank, same_device)
 
     if rank != 0:
         return
-    alg_bytes = st["alg_bytes"]   # this rank's launch (all ranks have equal shards by construction)
-    achieved = alg_bytes / (lin_ms * 1e-3) / 1e9
-    tr = load_traffic(args.config, views_per_rank) if world == 1 else None
+    tr = load_profile("traffic", args.config, views_per_rank) if world == 1 else None
+    rl = roofline(st, m["lin_ms"], tr)
+    rl["kernel_launches_timed"] = m["nlaunch"]
+    rl["step_ms_events"] = m["step_ms_ev"]
     out = {
         "metric": METRIC,
         "value": value,
@@ -233,29 +338,19 @@ def main():
             "transport": transport,
             "state_dtype": "f32", "jacobian_dtype": "f64",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "k_linearize",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": (tr["bytes_per_launch"] if tr else None),
-            "alg_bytes_per_launch": alg_bytes,
-            "alg_bytes_formula": "20 B/corner (float32 obj xyz + img uv) + 280 B/edge (SURVEY.md 8(d))",
-            "kernel_ms_per_launch": lin_ms,
-            "kernel_launches_timed": nlaunch,
-            "step_ms_events": step_ms_ev,
-        },
+        "clock_ramp": m["ramp"],
+        "roofline": rl,
     }
     fp = load_profile("fp64", args.config, views_per_rank) if world == 1 else None
     if fp and fp.get("fp64_flops_per_launch"):
-        tf = fp["fp64_flops_per_launch"] / (lin_ms * 1e-3) / 1e12
+        tf = fp["fp64_flops_per_launch"] / (m["lin_ms"] * 1e-3) / 1e12
         out["fp64_valu"] = {"achieved": tf, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFS,
                             "flops_per_launch": fp["fp64_flops_per_launch"],
                             "flops_per_corner": fp["fp64_flops_per_corner"],
                             "source": "profiles/fp64_*.json (rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, "
                                       "an upper bound) / the event-timed launch"}
+    if strong:
+        out["strong"] = strong
     if not args.no_parity and world == 1:
         from oracle import oracle_py as O
         o = O.Oracle(prob)
@@ -266,9 +361,11 @@ def main():
         out["parity"] = {"meanReProjError_gpu": mg, "meanReProjError_oracle": mr, "abs_diff_px": abs(mg - mr),
                          "iters_gpu": itg, "iters_oracle": itr,
                          "max_abs_param_diff": float(np.abs(xg - xr).max())}
+    if world == 1 and not args.no_extra:
+        out["configs"] = {name: config_line(name, device=local_rank) for name in ("config3", "config4", "config5")}
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(prob, args.cpu_seconds)
-    ba.close()
+        out["cpu_baseline_ref_faithful"] = cpu_baseline_ref_faithful()
     print(json.dumps(out))
 
 

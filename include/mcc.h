@@ -64,7 +64,9 @@ typedef struct mcc_problem mcc_problem;
  * 0..n_photos-1.  Edges are in reference order (_edgeList).  Parameters follow buildParas
  * (src/multicalib.cpp:422-440): [cam1..cam(C-1), photo0..] x (rvec, tvec), or for DOUBLESIDE
  * (src/doubleSide.cpp:233-261): [ds, photo0..].  n_photos >= 1 and n_edges >= 1 (MCC_EINVAL
- * otherwise: the reference's mean error is 0/0 without observations); at most 22 cameras
+ * otherwise: the reference's mean error is 0/0 without observations).  A camera without
+ * observations is accepted (a photo shard of a multi-GPU problem may lack one); if the whole
+ * problem leaves one unobserved the solve reports MCC_ENOTPD.  At most 22 cameras
  * (global block m <= 128, the reduced solve's LDS-resident matrix) and 1024 corners per edge. */
 typedef struct mcc_desc {
     int model;
@@ -105,7 +107,9 @@ int mcc_optimize(mcc_problem *p, int crit_type, int max_count, double eps, float
                  int *iters, double *last_change);
 
 /* n unconditional Gauss-Newton iterations on the device-resident parameters, enqueued
- * asynchronously (bench / throughput path).  Use mcc_synchronize to wait. */
+ * asynchronously (bench / throughput path).  Use mcc_synchronize to wait.  The first call after
+ * any other entry point switches the device state to free-running (one host round trip);
+ * back-to-back calls only enqueue. */
 int mcc_step(mcc_problem *p, int n);
 int mcc_synchronize(mcc_problem *p);
 

@@ -164,6 +164,9 @@ struct mcc_problem {
     static constexpr int kGraphSteps = 8;
     hipGraphExec_t gexec[2] = {nullptr, nullptr};
     bool use_graph = true;
+    // the device State is in free-running mode (crit_type 0) since the last mcc_step: later
+    // mcc_step calls enqueue without a host round trip (set_state clears it)
+    bool stepping = false;
 
     // RCCL
     ncclComm_t comm = nullptr;
@@ -345,6 +348,7 @@ int launch_update_steps(mcc_problem* p, int n) {
 int read_state(mcc_problem* p);
 
 int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, double eps) {
+    p->stepping = false;
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
     if (reset_iter) {
@@ -551,9 +555,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         block_items[b + 1] = (int)items.size();
     }
     p->n_pair_doubles = n_doubles;
-    for (int b1 = 0; b1 < nb; ++b1)
-        if (blk_src[blk_index(b1, b1)].empty())
-            return bail(fail(MCC_EINVAL, "global block " + std::to_string(b1) + " has no observations"));
+    // A camera block without an observation here is accepted: a rank of a photo-sharded problem
+    // may hold no photo of some camera while the summed system is fine.  If the whole problem
+    // leaves a camera unobserved, the reduced system is singular and the step fails with
+    // MCC_ENOTPD (the device positive-definiteness check of the solve).
     p->n_items = (int)items.size();
     p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
@@ -752,9 +757,14 @@ int mcc_optimize(mcc_problem* p, int crit_type, int max_count, double eps, float
 int mcc_step(mcc_problem* p, int n) {
     if (!p || n < 0) return fail(MCC_EINVAL, "bad argument");
     HIPCHK(hipSetDevice(p->device));
-    // crit_type 0: every step updates (no stop test), iteration counter keeps running
-    int rc = set_state(p, 0, 0, 0, 0.0);
-    if (rc) return rc;
+    // crit_type 0: every step updates (no stop test), iteration counter keeps running.  Only the
+    // first call after another entry point touched the state syncs and rewrites it; back-to-back
+    // calls just enqueue (no host round trip inside a timed window of steps)
+    if (!p->stepping) {
+        int rc = set_state(p, 0, 0, 0, 0.0);
+        if (rc) return rc;
+        p->stepping = true;
+    }
     return launch_update_steps(p, n);
 }
 

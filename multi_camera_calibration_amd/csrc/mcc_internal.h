@@ -92,7 +92,7 @@ struct LinArgs {
 
 struct SchurArgs {
     State* state;
-    const int4* items;   // {block, pair_begin, pair_end, -}
+    const int4* items;   // {camera-pair block, first slot's offset in doubles, slot count, slot size 48 | 36}
     const double* pairprod;   // 48 (diagonal block) or 36 doubles per pair, written by k_linearize, block-major
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;

@@ -1802,7 +1802,8 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 }
 
 // ---------------------------------------------------------------- k_schur
-// Work item: slots [begin, end) of one camera-pair block.  k_linearize wrote each pair's product
+// Work item {block, offset of its first slot in doubles, slot count, slot size 48 | 36}: a run of
+// consecutive slots of one camera-pair block.  k_linearize wrote each pair's product
 // at its slot (48 doubles: [self] Hgg_a - Y'_a Hgp_b^T, [self] (gg_a - Y'_a gp), [self] gg_a; 36 on an
 // off-diagonal block, which has no self pair), so an
 // item streams and sums them.  Thread t < 240: entry q = t % 48 (0..35: S entry, 36..41: r entry,

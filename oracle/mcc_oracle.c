@@ -937,6 +937,54 @@ int ora_photo_backsub(const ora_problem *p, const float *x, int lo, int hi, cons
     return rc;
 }
 
+int ora_normal_dense_j(const ora_problem *p, const float *x, double *JTJ, double *JTE)
+{
+    /* src/mymulticalib.cpp:680-803 literally, one thread: J = zeros(2 sum N, P) (:683), each
+     * edge's 2N x 6 blocks copied in at the camera / photo columns (:776-786), E stacked (:784),
+     * then JTJ = J.t() * J and JTE = J.t() * E as dense products (:802-803).  The product runs
+     * over the transpose (P rows of length 2 sum N), so each entry is one contiguous dot. */
+    int P = ora_nparams(p);
+    long long rows = 0;
+    int maxn = 0;
+    for (int e = 0; e < p->n_edges; ++e) {
+        rows += 2LL * p->edge_n[e];
+        if (p->edge_n[e] > maxn) maxn = p->edge_n[e];
+    }
+    double *Jt = (double *)calloc((size_t)P * (size_t)rows, sizeof(double));
+    double *E = (double *)malloc(sizeof(double) * (size_t)rows);
+    double *jc = (double *)malloc(sizeof(double) * 12 * (size_t)maxn);
+    double *jp = (double *)malloc(sizeof(double) * 12 * (size_t)maxn);
+    int rc = 0;
+    if (!Jt || !E || !jc || !jp) { rc = -3; goto out; }
+    long long r0 = 0;
+    for (int e = 0; e < p->n_edges; ++e) {
+        if ((rc = ora_edge_linearize(p, x, e, jc, jp, E + r0, NULL))) goto out;
+        int gc = global_col(p, e), pc = ora_param_col_photo(p, p->edge_photo[e]);
+        for (int r = 0; r < 2 * p->edge_n[e]; ++r)
+            for (int j = 0; j < 6; ++j) {
+                if (gc >= 0) Jt[(size_t)(gc + j) * rows + r0 + r] = jc[r * 6 + j];
+                Jt[(size_t)(pc + j) * rows + r0 + r] = jp[r * 6 + j];
+            }
+        r0 += 2LL * p->edge_n[e];
+    }
+    for (int a = 0; a < P; ++a) {
+        const double *ja = Jt + (size_t)a * rows;
+        for (int b = a; b < P; ++b) {
+            const double *jb = Jt + (size_t)b * rows;
+            double s = 0;
+            for (long long r = 0; r < rows; ++r) s += ja[r] * jb[r];
+            JTJ[(size_t)a * P + b] = s;
+            JTJ[(size_t)b * P + a] = s;
+        }
+        double s = 0;
+        for (long long r = 0; r < rows; ++r) s += ja[r] * E[r];
+        JTE[a] = s;
+    }
+out:
+    free(Jt); free(E); free(jc); free(jp);
+    return rc;
+}
+
 int ora_linearize_solve(const ora_problem *p, const float *x, int solver, double *delta,
                         double *jte)
 {
@@ -945,7 +993,7 @@ int ora_linearize_solve(const ora_problem *p, const float *x, int solver, double
     double *JTJ = (double *)malloc(sizeof(double) * (size_t)P * P);
     double *JTE = (double *)malloc(sizeof(double) * (size_t)P);
     if (!JTJ || !JTE) { free(JTJ); free(JTE); return -3; }
-    int rc = ora_normal_dense(p, x, JTJ, JTE);
+    int rc = solver == ORA_SOLVER_DENSE_J ? ora_normal_dense_j(p, x, JTJ, JTE) : ora_normal_dense(p, x, JTJ, JTE);
     if (!rc) {
         ora_cg(P, JTJ, JTE, delta);
         if (jte) memcpy(jte, JTE, sizeof(double) * (size_t)P);

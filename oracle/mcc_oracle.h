@@ -38,7 +38,7 @@ extern "C" {
 
 enum { ORA_PINHOLE = 0, ORA_OMNI = 1, ORA_DOUBLESIDE = 2 };
 enum { ORA_FRONT = 0, ORA_BACK = 1 };
-enum { ORA_SOLVER_CG = 0, ORA_SOLVER_SCHUR = 1 };
+enum { ORA_SOLVER_CG = 0, ORA_SOLVER_SCHUR = 1, ORA_SOLVER_DENSE_J = 2 };
 
 typedef struct ora_problem {
     int model;              /* ORA_PINHOLE (MyMulti), ORA_OMNI (base class), ORA_DOUBLESIDE   */
@@ -92,12 +92,19 @@ int ora_edge_linearize(const ora_problem *p, const float *x, int e,
 /* Dense faithful normal equations (J is (2*corners) x P, as src/mymulticalib.cpp:683). */
 int ora_normal_dense(const ora_problem *p, const float *x, double *JTJ, double *JTE);
 
+/* The same normal equations the way the reference forms them: a materialised dense J
+ * ((2*corners) x P, zero-filled) and the dense products J^T J, J^T E (src/mymulticalib.cpp:683,
+ * 802-803), single-threaded -- the ref-faithful CPU baseline's cost model. */
+int ora_normal_dense_j(const ora_problem *p, const float *x, double *JTJ, double *JTE);
+
 /* Eigen ConjugateGradient<Lower|Upper, DiagonalPreconditioner>, tol = eps, maxIter = 2P,
  * solve() called twice as in src/multicalib.cpp:571-577. Returns iterations of last solve. */
 int ora_cg(int P, const double *A, const double *b, double *x);
 
 /* One linearisation + solve (the computeJacobianExtrinsic seam).  solver ORA_SOLVER_CG is the
- * faithful dense path, ORA_SOLVER_SCHUR the exact block-sparse Schur/Cholesky solve. */
+ * faithful dense path (dense J^T J accumulated per edge + CG x2), ORA_SOLVER_DENSE_J the same with
+ * the materialised dense J and gemm products, ORA_SOLVER_SCHUR the exact block-sparse
+ * Schur/Cholesky solve. */
 int ora_linearize_solve(const ora_problem *p, const float *x, int solver,
                         double *delta, double *jte);
 

@@ -47,6 +47,12 @@ def lib():
     return _LIB
 
 
+# ora_linearize_solve solvers: "cg" = dense J^T J (accumulated per edge) + Eigen-CG x2,
+# "dense_j" = the same from a materialised dense J with gemm products (the reference's cost),
+# "schur" = exact block-sparse Schur solve
+SOLVERS = {"cg": 0, "schur": 1, "dense_j": 2}
+
+
 def _p(a, t):
     return a.ctypes.data_as(t) if a is not None else None
 
@@ -105,7 +111,7 @@ class Oracle:
     def linearize_solve(self, x, solver="schur"):
         x = np.ascontiguousarray(x, np.float32)
         d = np.zeros(self.P); jte = np.zeros(self.P)
-        rc = lib().ora_linearize_solve(ctypes.byref(self.s), _p(x, _f32p), 1 if solver == "schur" else 0,
+        rc = lib().ora_linearize_solve(ctypes.byref(self.s), _p(x, _f32p), SOLVERS[solver],
                                        _p(d, _f64p), _p(jte, _f64p))
         if rc:
             raise RuntimeError(f"ora_linearize_solve failed: {rc}")
@@ -133,7 +139,7 @@ class Oracle:
         x = np.array(x, np.float32, copy=True)
         it = ctypes.c_int(0); ch = ctypes.c_double(0)
         mean = lib().ora_optimize(ctypes.byref(self.s), crit_type, max_count, ctypes.c_double(eps),
-                                  1 if solver == "schur" else 0, _p(x, _f32p), ctypes.byref(it),
+                                  SOLVERS[solver], _p(x, _f32p), ctypes.byref(it),
                                   ctypes.byref(ch))
         if mean < 0:
             raise RuntimeError("ora_optimize failed")

@@ -23,12 +23,21 @@ CASES = {
     "config5_small": lambda: rig.make_config("config5", n_views=24),
     # m = 90: k_linearize + k_schur, the exchange runs in k_solve
     "config3_small": lambda: rig.make_config("config3", n_views=48),
+    # a shard without any observation of one camera (config2, 40 views, camera 3 on rank 0 only)
+    "config2_nocam": lambda: rig.make_config("config2", n_views=40),
+    # BASELINE.json's multi-GPU rigs at full size (bench.py's strong-scaling lines)
+    "config3_full": lambda: rig.make_config("config3"),
+    "config5_full": lambda: rig.make_config("config5"),
 }
 
 
 def shard(case, world, rank):
     p = CASES[case]()
     owner = api.partition_photos(p, world)
+    if case == "config2_nocam":
+        # every photo camera 3 observes goes to rank 0: the other ranks' shards have no edge of
+        # camera block 2 (their local reduced system is singular, the summed one is not)
+        owner[np.unique(p.edge_photo[p.edge_cam == 3])] = 0
     mine = np.nonzero(owner == rank)[0]
     return p, mine, rig.subset_photos(p, mine)
 

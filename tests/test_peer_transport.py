@@ -58,10 +58,14 @@ def _run_ranks(case, world, tmp_path, steps=100):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["config2_small", "config5_small", "config3_small"])
+@pytest.mark.parametrize("case", ["config2_small", "config5_small", "config3_small", "config2_nocam", "config3_full",
+                                  "config5_full"])
 def test_peer_two_ranks_one_device(case, tmp_path):
+    """*_full: BASELINE.json's multi-GPU rigs (config3: 16 cameras x 5k views, m = 90; config5:
+    8-camera double-sided board x 2k views) at their fixed size split over two ranks -- the
+    strong-scaling split bench.py measures at N > 1."""
     world = 2
-    outs = _run_ranks(case, world, tmp_path)
+    outs = _run_ranks(case, world, tmp_path, steps=20 if case.endswith("_full") else 100)
     p = peer_worker.CASES[case]()
     m = p.global_dim
     ba = api.BundleAdjuster(p)

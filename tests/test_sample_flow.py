@@ -347,3 +347,71 @@ def test_omni_base_class_flow(sample, tmp_path):
     assert np.abs(xg[:, 3:] - xo6[:, 3:]).max() <= 1e-5 * max(1.0, np.abs(xo6[:, 3:]).max())
     root = ET.parse(out).getroot()
     assert root.find("xi_0") is not None and root.find("nCameras").text.strip() == str(p.n_cams)
+
+
+STEREO_FIXTURE = os.path.join(ROOT, "tests", "golden", "tutorial_stereo_v20.npz")
+
+
+def _write_corner_file(path, img, obj, size):
+    n = len(img)
+    with open(path, "w") as f:
+        f.write("%YAML:1.0\n---\n")
+        f.write(f"imagePoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"2f\"\n   data: [ "
+                + ", ".join(repr(float(v)) for v in np.asarray(img, np.float32).ravel()) + " ]\n")
+        f.write(f"objectPoints: !!opencv-matrix\n   rows: {n}\n   cols: 1\n   dt: \"3f\"\n   data: [ "
+                + ", ".join(repr(float(v)) for v in np.asarray(obj, np.float32).ravel()) + " ]\n")
+        f.write(f"imageSize: [ {int(size[0])}, {int(size[1])} ]\n")
+
+
+@pytest.mark.gpu
+def test_tutorial_stereo_real_corners(sample, tmp_path):
+    """REAL corners through the base-class flow on the GPU: the first 20 views of the reference's
+    tutorials/data/omni_stereocalib_data.xml (2 omnidirectional cameras; the corner arrays travel
+    in the committed fixture tests/golden/tutorial_stereo_v20.npz) as "camera-timestamp" corner
+    files -> MultiCameraCalibration(OMNIDIRECTIONAL, 2, list) loadImages (GPU omnidir calibrate
+    per camera) -> initialize -> optimizeExtrinsics (GPU, TermCriteria(COUNT, 20, 1e-7)).
+    Against the fixture, which the CPU oracle made along the same flow: the same edges and photo
+    vertices, intrinsics and initial poses to the oracle calibration's rounding, and the GPU
+    optimisation equal to the oracle's from the sample's own initial vector."""
+    g = dict(np.load(STEREO_FIXTURE))
+    size = tuple(int(v) for v in g["meta"][3:5])
+    root = tmp_path / "stereo"
+    os.makedirs(root)
+    names = ["pattern.png"]
+    for c, key in enumerate(("raw_img1", "raw_img2")):
+        for i in range(g[key].shape[0]):
+            name = f"{c}-{i}.yaml"
+            _write_corner_file(root / name, g[key][i], g["raw_obj"][i], size)
+            names.append(name)
+    lst = root / "images.yaml"
+    lst.write_text("%YAML:1.0\n---\nimages:\n" + "".join(f"   - {nm}\n" for nm in names))
+    dump, res, out = str(tmp_path / "p.bin"), str(tmp_path / "r.txt"), str(tmp_path / "res.xml")
+    _run(sample, ["--list", str(lst), "--omni", "--cameras", "2", "--min-matches", "20",
+                  "--dump-problem", dump, "--dump-result", res, "--out", out])
+    q, ts = SD.read_dump(dump)
+    p = rig.problem_from_arrays(g)
+    # the problem loadImages + initialize built: same kept views, edges, photo vertices, points
+    for f in ("edge_cam", "edge_photo", "edge_off", "edge_n"):
+        assert np.array_equal(getattr(q, f), getattr(p, f)), f
+    assert list(ts) == list(p.timestamps)
+    assert np.array_equal(q.obj, p.obj) and np.array_equal(q.img, p.img)
+    # intrinsics: GPU calibrate vs the oracle restatement (300 iterations each, float32 stored)
+    for c in range(2):
+        assert np.allclose(q.K[c], p.K[c], rtol=1e-4, atol=1e-3), (c, q.K[c], p.K[c])
+        assert abs(float(q.xi[c]) - float(p.xi[c])) <= 1e-4 * abs(float(p.xi[c])), c
+        assert np.allclose(q.D[c], p.D[c], rtol=1e-3, atol=1e-6), (c, q.D[c], p.D[c])
+    x0q = q.x0.reshape(-1, 6).astype(np.float64)
+    x0p = p.x0.reshape(-1, 6).astype(np.float64)
+    for a, b in zip(x0q, x0p):
+        assert np.abs(_rot(a[:3]) - _rot(b[:3])).max() <= 1e-3
+    assert np.abs(x0q[:, 3:] - x0p[:, 3:]).max() <= 1e-3 * np.abs(x0p[:, 3:]).max()
+    # the GPU optimisation from the sample's own problem equals the oracle's (both solvers)
+    r = SD.read_result(res)
+    o = O.Oracle(q)
+    for solver in ("schur", "cg"):
+        xo, mo, ito, _ = o.optimize(q.x0, crit_type=1, max_count=20, eps=1e-7, solver=solver)
+        assert r["iterations"] == ito == 20
+        assert abs(r["error"] - mo) <= 1e-6, (solver, r["error"], mo)
+    assert abs(r["error"] - float(g["mean_opt"])) <= 1e-3   # same data, seeds from two calibrations
+    root_xml = ET.parse(out).getroot()
+    assert root_xml.find("xi_1") is not None and root_xml.find("nCameras").text.strip() == "2"
