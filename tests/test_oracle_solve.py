@@ -77,3 +77,26 @@ def test_step_factor_and_float32_state(cfg2):
         x = (x + G).astype(np.float32)
     x2, _, _, _ = o.optimize(p.x0, 1, 2, 0.0)
     assert np.array_equal(x, x2)
+
+
+def test_final_iterate_float32_sensitivity():
+    """Why the full-size GPU parity bar on the parameters is the float32 resolution of the state
+    and not a per-parameter ulp count: the reference's loop (src/multicalib.cpp:462-514, float32
+    x, G = fl32(0.95^(k+1) delta)) is itself chaotic at float32 rounding.  Flipping ONE x0 entry
+    by one ulp leaves the iteration count and the mean error (to < 1e-6 px) unchanged, but moves
+    hundreds of final parameters, the small ones by hundreds of ulps; the move stays within a
+    couple of float32 spacings of the largest rotation / translation."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ulp import f32_ulp_diff, state_resolution_diff
+    p = rig.make_config("config2")
+    o = O.Oracle(p)
+    x1, m1, i1, _ = o.optimize(p.x0, 3, 200, 1e-7)
+    x0b = p.x0.copy()
+    k = p.global_dim + 3                              # the first photo's tvec x
+    x0b[k] = np.nextafter(x0b[k], np.float32(np.inf))
+    x2, m2, i2, _ = o.optimize(x0b, 3, 200, 1e-7)
+    u = f32_ulp_diff(x1, x2)
+    assert i1 == i2 and abs(m1 - m2) <= 1e-6
+    assert (u > 0).sum() > 100 and u.max() > 100      # far beyond a per-parameter ulp bar
+    assert state_resolution_diff(x1, x2) <= 2.0
