@@ -52,6 +52,13 @@ struct Node {
     int toInt() const;
 };
 
+// Path remapping for callers that hard-code their data and config locations (the reference
+// sample does: samples/multi_cameras_calibration.cpp:50-52).  MCC_PATH_MAP="from=to[;from=to...]"
+// rewrites a path that starts with `from` (the first matching entry, once) to start with `to`;
+// without the variable a path is returned unchanged.  Every file the loaders and writers open and
+// every folder they list goes through it.
+std::string resolve_path(const std::string& path);
+
 class FileStorage {
 public:
     enum { READ = 0, WRITE = 1 };

@@ -57,6 +57,10 @@ _LIB = None
 HOST_LIB_PATH = os.path.join(_HERE, "libmcc_host.so")
 SAMPLE_PATH = os.path.join(_HERE, "build", "multi_cameras_calibration")
 OMNI_SAMPLE_PATH = os.path.join(_HERE, "build", "omni_calibration")
+# the reference's samples/multi_cameras_calibration.cpp compiled unchanged against
+# include/opencv2/ccalib/*.hpp (built only where the reference tree exists; the binary travels)
+REF_SAMPLE_SRC = "/root/reference/samples/multi_cameras_calibration.cpp"
+REF_SAMPLE_PATH = os.path.join(_HERE, "build", "ref_multi_cameras_calibration")
 
 
 def build(force: bool = False) -> str:
@@ -70,6 +74,8 @@ def build(force: bool = False) -> str:
         os.path.getmtime(s) > min(os.path.getmtime(o) for o in outs) for s in srcs)
     if force or stale:
         subprocess.run(["make", "-s", "--no-print-directory", "-C", _HERE, "-j4", "all"], check=True)
+    if os.path.exists(REF_SAMPLE_SRC):
+        subprocess.run(["make", "-s", "--no-print-directory", "-C", _HERE, "ref_sample"], check=True)
     return LIB_PATH
 
 

@@ -362,7 +362,7 @@ void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers)
     if (!outliers.empty()) m_outliers = outliers;
     const int backN = _BackPatternSize.width * _BackPatternSize.height;
     for (int cam = 0; cam < _nCamera; ++cam) {   // loadOneSerial (src/mymulticalib.cpp:262-301)
-        const std::string folder = dataFolder + "/" + cameraSerials[cam];
+        const std::string folder = stg::resolve_path(dataFolder + "/" + cameraSerials[cam]);
         std::vector<std::string> files;
         if (fsys::is_directory(folder))
             for (const auto& de : fsys::directory_iterator(folder))

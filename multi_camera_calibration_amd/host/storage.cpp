@@ -370,7 +370,27 @@ int Node::toInt() const {
     throw std::runtime_error("FileStorage node is not a number");
 }
 
-FileStorage::FileStorage(const std::string& path, int flags) : path_(path), flags_(flags) {
+std::string resolve_path(const std::string& path) {
+    const char* env = std::getenv("MCC_PATH_MAP");
+    if (!env || !*env) return path;
+    const std::string map(env);
+    size_t pos = 0;
+    while (pos <= map.size()) {
+        size_t end = map.find(';', pos);
+        if (end == std::string::npos) end = map.size();
+        const std::string item = map.substr(pos, end - pos);
+        const size_t eq = item.find('=');
+        if (eq != std::string::npos && eq > 0) {
+            const std::string from = item.substr(0, eq), to = item.substr(eq + 1);
+            if (path.compare(0, from.size(), from) == 0) return to + path.substr(from.size());
+        }
+        pos = end + 1;
+    }
+    return path;
+}
+
+FileStorage::FileStorage(const std::string& path_in, int flags) : path_(resolve_path(path_in)), flags_(flags) {
+    const std::string& path = path_;
     xml_ = !(ends_with(path, ".yml") || ends_with(path, ".yaml"));
     if (flags == WRITE) {
         std::ofstream probe(path, std::ios::app);

@@ -35,13 +35,19 @@ def outlier_noise(e: int, n: int, px: float) -> np.ndarray:
     return np.random.default_rng(1000 + e).normal(size=(n, 2)) * px
 
 
-def write_dataset(p: "rig.Problem", root: str, outlier_edges=(), outlier_px=2.0, back_views=0, ts0=100000):
+def write_dataset(p: "rig.Problem", root: str, outlier_edges=(), outlier_px=2.0, back_views=0, ts0=100000,
+                  serials=None, ds_config=None):
     """Writes p's views as corner files (one per edge) and camera configs under root.
     outlier_edges: edge indices whose corners get outlier_noise(e, n, outlier_px) (outliers for
     pass 1);
     back_views: extra 70-corner files per camera (back-pattern views the loader must drop).
+    serials: camera serial names (default cam00, cam01, ...); ds_config: also write the rig's
+    double-side transform there (key "transform", src/mymulticalib.cpp:99-103).
     Returns (serials, data dir, config dir, {file: edge}, timestamps of the rig's photos)."""
-    serials = [f"cam{c:02d}" for c in range(p.n_cams)]
+    serials = list(serials) if serials is not None else [f"cam{c:02d}" for c in range(p.n_cams)]
+    if ds_config is not None:
+        with open(ds_config, "w") as f:
+            f.write("%YAML:1.0\n---\n" + _mat_yaml("transform", p.ds_pose))
     data, config = os.path.join(root, "data"), os.path.join(root, "config")
     os.makedirs(config, exist_ok=True)
     for c, s in enumerate(serials):
