@@ -142,6 +142,9 @@ struct mcc_problem {
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
+    // m > 30 (or MCC_FUSED=0): the split step k_prep -> k_edge -> k_photo (MCC_SPLIT=0: the
+    // earlier single per-photo k_linearize)
+    int split = 1;
     int max_cpp = 1;   // most corners of one photo
     hipStream_t stream = nullptr;
 
@@ -154,6 +157,7 @@ struct mcc_problem {
     DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
+    DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk, photo_pair_ptr;
     DevBuf<int4> edge_info, items, photo_pairs;
     DevBuf<State> state;
@@ -249,7 +253,14 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p; la.W = p->W.p;
     la.solve = solve_ctx(p, do_update);
     la.solve.stamps = nullptr;
-    if (p->V > 0) HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
+    la.n_edges = p->E; la.n_photos = p->V;
+    la.erec = p->erec.p; la.echain = p->echain.p; la.eh = p->eh.p;
+    if (p->V > 0) {
+        if (!p->fused && p->split)
+            HIPCHK(mcc_launch_split(la, p->model, p->max_epp, p->max_ppp, p->rational, p->prism, p->stream));
+        else
+            HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
+    }
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
     if (p->fused) {
         if (rccl) {
@@ -566,6 +577,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // small camera blocks: one kernel per Gauss-Newton step (MCC_FUSED=0 forces the k_schur path)
     p->fused = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
     if (const char* f = std::getenv("MCC_FUSED")) p->fused = p->fused && std::atoi(f) != 0;
+    if (const char* f = std::getenv("MCC_SPLIT")) p->split = std::atoi(f) != 0;
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;
 
@@ -618,6 +630,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E));
     HIPC(p->pairprod.alloc(p->fused ? 0 : p->n_pair_doubles));
+    const bool use_split = !p->fused && p->split;
+    HIPC(p->erec.alloc(use_split ? 12 * (size_t)E : 0));
+    HIPC(p->echain.alloc(use_split ? 54 * (size_t)E : 0));
+    HIPC(p->eh.alloc(use_split ? 90 * (size_t)E : 0));
     HIPC(p->zp.alloc(6 * (size_t)V));
     HIPC(p->gp_tot.alloc(6 * (size_t)V));
     // + 24 zeroed items of padding: the assembly loads a fixed 24 items per block unconditionally
@@ -675,6 +691,7 @@ void mcc_destroy(mcc_problem* p) {
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
+    p->erec.release(); p->echain.release(); p->eh.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();

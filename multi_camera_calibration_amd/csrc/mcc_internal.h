@@ -88,7 +88,18 @@ struct LinArgs {
     double* W;               // [V * 6m] per-photo pending-update matrix (next step's phase 0)
     SolveCtx solve;
     PeerCtx peer;            // nranks > 0: the final arriver exchanges with the peers and solves
+    // split step (m > 30): k_prep -> k_edge -> k_photo
+    int n_edges, n_photos;
+    double* erec;            // [12E] R (9), T (3) of the float32 composed pose (k_prep -> k_edge)
+    double* echain;          // [54E] chain-map blocks Gp11, Gp21, Gp22, Gg11, Gg21, Gg22 (k_prep -> k_edge)
+    double* eh;              // [90E] Hpp upper (21), Hgg upper (21), Hgp (36), gp (6), gg (6) (k_edge -> k_photo)
 };
+
+// k_photo's LDS: Hgp, Y' [ne][36], Hgg [ne][21], gg [ne][6], Hpp, Hpp^-1 [36], gp [6], gblock
+// [ne] ints, then (16-B aligned) the photo's Schur pairs
+__host__ __device__ inline size_t photo_lds_doubles(int ne) {
+    return ((size_t)99 * ne + 78 + (size_t)(ne + 1) / 2 + 1) & ~(size_t)1;
+}
 
 struct SchurArgs {
     State* state;
@@ -143,6 +154,9 @@ struct ErrArgs {
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp);
 size_t mcc_solve_shmem(int m);
 hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp, int max_ppp);
+size_t mcc_photo_shmem(int max_epp, int max_ppp);
+hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, int max_epp, int max_ppp, bool rational, bool prism,
+                            hipStream_t s);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);

@@ -1464,6 +1464,506 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     RSTAMP(15);
 }
 
+// ================================================================ split step (m > 30)
+// The large-m step as three kernels, each over its natural unit, so that no workgroup carries a
+// long serial chain at low occupancy ("split step"):
+//   k_prep   one 16-lane group per photo vertex: the previous step's pending photo update, then
+//            one LANE per edge: photo / camera Rodrigues, compose_motion (+ the double-side compose
+//            of BACK edges), the float32 composed pose and its Rodrigues, the chain maps ->
+//            per-edge records erec (R, T) and echain (Gp, Gg blocks);
+//   k_edge   L lanes per edge (64 / L edges per wave): the corner sweep (FP64 projection + 2x6
+//            J' rows, float32 residual), the L-lane butterfly of the 27 normal-equation sums, and
+//            the chain H = G^T A' G, g = G^T b' -> eh;
+//   k_photo  one wave per photo vertex: Hpp = sum_e Hpp_e, its inverse, z', the Schur factors
+//            Y'_e = Hgp_e Hpp^-1 and the photo's Schur pair products (k_schur sums them).
+// (src/mymulticalib.cpp:468-614, 668-818; src/multicalib.cpp:593-824; src/doubleSide.cpp:288-581)
+
+// float32 composed pose -> R (Rodrigues of the float32 vector, for the projection), T, Jl(fl32 om)
+__device__ __forceinline__ void prep_finish(const double* om, const double* Tc, double th, double sn, double cs,
+                                            double* R, double* T, double* Jl) {
+    double rf[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)om[k]; T[k] = (double)(float)Tc[k]; }   // :546-553
+    Rot rp;
+    rodrigues_near(rf, th, sn, cs, rp);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = rp.R[k];
+    so3_jac(rf, rp, +1.0, Jl);
+}
+
+// One edge's prologue (one lane).  gb: the chain maps' nonzero 3x3 blocks, row-major:
+// [0..26]  Gp11, Gp21, Gp22 with Gp = [[Gp11, 0], [Gp21, Gp22]] (photo: J_photo = J' Gp)
+// [27..53] Gg11, Gg21, Gg22 with Gg likewise (camera or double-side block)
+template <int MODEL>
+__device__ __forceinline__ void prep_edge(const double* R1, const double* Jr1, const double* T1, const double* R2,
+                                          const double* Jl2, const double* T2, const double* Rds, const double* Jrds,
+                                          const double* dst, int side, double* er, double* gb) {
+    double* R = er;
+    double* T = er + 9;
+    Motion f;
+    double th3, s3, c3;
+    compose(R1, Jr1, T1, R2, Jl2, T2, f, th3, s3, c3);   // compose_motion(photo, camera), :498-500
+    double Jl[9], t9[9];
+    if (side == MCC_BACK) {
+        // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506 / src/doubleSide.cpp:320-322;
+        // R(om_front) is the FP64 composed rotation itself (Rodrigues(om_front) to rounding)
+        Rot rf0;
+        rf0.th = th3; rf0.s = s3; rf0.c = c3;
+        double Jlf[9];
+        so3_jac(f.om, rf0, +1.0, Jlf);
+        Motion b;
+        double th, sn, cs;
+        compose(Rds, Jrds, dst, f.R, Jlf, f.T, b, th, sn, cs);
+        prep_finish(b.om, b.T, th, sn, cs, R, T, Jl);
+        mat3_mul(b.A2, f.A1, t9);          // photo: [[Jl A2b A1, 0], [B2b A1, R2]]  (:509-512)
+        mat3_mul(Jl, t9, gb);
+        mat3_mul(b.B2, f.A1, gb + 9);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) gb[18 + k] = R2[k];
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {   // ds block: [[Jl A1b, 0], [0, R_front]]  (doubleSide.cpp:398-399)
+            mat3_mul(Jl, b.A1, gb + 27);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { gb[36 + k] = 0.0; gb[45 + k] = f.R[k]; }
+        } else {   // camera block as the reference chains it, omitting dTt/dTf dTf/dRc (:516, hazard A12)
+            mat3_mul(b.A2, f.A2, t9);
+            mat3_mul(Jl, t9, gb + 27);
+            mat3_mul(b.B2, f.A2, gb + 36);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) gb[45 + k] = (k % 4 == 0) ? 1.0 : 0.0;
+        }
+    } else {
+        prep_finish(f.om, f.T, th3, s3, c3, R, T, Jl);
+        mat3_mul(Jl, f.A1, gb);             // photo: [[Jl A1, 0], [0, R2]]
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { gb[9 + k] = 0.0; gb[18 + k] = R2[k]; }
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {   // front edges carry a zero ds block (doubleSide.cpp:335-336)
+#pragma unroll
+            for (int k = 0; k < 27; ++k) gb[27 + k] = 0.0;
+        } else {                               // camera: [[Jl A2, 0], [B2, I]]
+            mat3_mul(Jl, f.A2, gb + 27);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { gb[36 + k] = f.B2[k]; gb[45 + k] = (k % 4 == 0) ? 1.0 : 0.0; }
+        }
+    }
+}
+
+constexpr int kPrepGroup = 16;   // lanes per photo vertex in k_prep (4 photos per wave)
+template <int MODEL>
+__global__ __launch_bounds__(64) void k_prep(LinArgs a) {
+    const State* st = a.state;
+    if (st->done) return;
+    const int tid = threadIdx.x, grp = tid / kPrepGroup, l = tid % kPrepGroup;
+    const int photo = blockIdx.x * (64 / kPrepGroup) + grp;
+    __shared__ double s_v[64 / kPrepGroup][16];
+    const bool valid = photo < a.n_photos;
+    const int e0 = valid ? a.photo_ptr[photo] : 0;
+    const int ne = valid ? a.photo_ptr[photo + 1] - e0 : 0;
+    const int pending = st->pending;
+    const double alpha_prev = st->alpha;   // step factor of the pending update
+    float* xg = a.x + a.global_dim + 6 * (size_t)photo;
+    // ---- the previous step's photo update, lane k < 6: dp_k = z'_k - sum_e (Y'_e^T dg_g(e))_k in
+    // edge order (k_backsub's photo_delta), G = fl32(alpha dp), x = fl32(x + G)
+    double xk = 0.0, Gk = 0.0;
+    if (valid && l < 6) {
+        const float xo = xg[l];
+        float xn = xo;
+        if (pending) {
+            double t = a.zp[6 * (size_t)photo + l];
+            for (int le = 0; le < ne; ++le) {
+                const int g = a.gblock[e0 + le];
+                if (g < 0) continue;
+                const double* Ye = a.Y + 36 * (size_t)(e0 + le) + l;
+                const double* d = a.dg + 6 * g;
+                double s = 0.0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) s += Ye[6 * i] * d[i];
+                t -= s;
+            }
+            const float G = (float)(alpha_prev * t);   // G = alpha*delta -> CV_32F (:491-496)
+            xn = xo + G;                                // x = x + G (:501)
+            xg[l] = xn;
+            Gk = (double)G;
+        }
+        xk = (double)xn;
+    }
+    if (l < 6) {
+        s_v[grp][l] = xk;
+        s_v[grp][8 + l] = Gk;
+    }
+    wave_sync_lds();
+    if (!valid) return;
+    if (pending && l == 0) {   // ||G||^2, ||x||^2 partials of the applied update (stop test)
+        double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            g2 += s_v[grp][8 + q] * s_v[grp][8 + q];
+            x2 += s_v[grp][q] * s_v[grp][q];
+        }
+        a.photo_norm[2 * (size_t)photo] = g2;
+        a.photo_norm[2 * (size_t)photo + 1] = x2;
+    }
+    // ---- photo Rodrigues (every lane of the group), the double-side transform
+    const double om1[3] = {s_v[grp][0], s_v[grp][1], s_v[grp][2]};
+    const double T1[3] = {s_v[grp][3], s_v[grp][4], s_v[grp][5]};
+    Rot r1;
+    rodrigues_v2m(om1, r1);
+    double Jr1[9];
+    so3_jac(om1, r1, -1.0, Jr1);
+    double Rds[9], Jrds[9], dst[3];
+    if (a.has_back) {
+        double dsr[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            dsr[k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[k] : a.ds_rt[k];
+            dst[k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[3 + k] : a.ds_rt[3 + k];
+        }
+        Rot rd;
+        rodrigues_v2m(dsr, rd);
+        so3_jac(dsr, rd, -1.0, Jrds);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rds[k] = rd.R[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rds[k] = Jrds[k] = 0.0;
+        dst[0] = dst[1] = dst[2] = 0.0;
+    }
+    // ---- one lane per edge
+    for (int le = l; le < ne; le += kPrepGroup) {
+        const int e = e0 + le;
+        const int4 info = a.edge_info[e];
+        const int cam = info.x;
+        double om2[3], T2[3];
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * cam + k]; T2[k] = a.cam_rt[6 * cam + 3 + k]; }
+        } else if (cam == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { om2[k] = a.x[6 * (cam - 1) + k]; T2[k] = a.x[6 * (cam - 1) + 3 + k]; }
+        }
+        Rot r2;
+        rodrigues_v2m(om2, r2);
+        double Jl2[9];
+        so3_jac(om2, r2, +1.0, Jl2);
+        prep_edge<MODEL>(r1.R, Jr1, T1, r2.R, Jl2, T2, Rds, Jrds, dst, info.y, a.erec + 12 * (size_t)e,
+                         a.echain + 54 * (size_t)e);
+    }
+}
+
+// Reduce-scatter butterfly of 32 per-lane values over a group of L lanes (L = 16 or 8: one DPP
+// row or half of one), fixed order: afterwards lane sub holds the full group sums of value
+// indices base + q (q < 32 / L), base = sum over the group's lane bits d of (sub & d ? 16 d / L * ... )
+template <int L>
+__device__ __forceinline__ void group_reduce_scatter(double* v, int lane) {
+    static_assert(L == 16 || L == 8, "group size");
+    int c = 32;
+    if (L == 16) {   // xor 8: rotate a row by 8
+        const bool hi = (lane & 8) != 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const double send = hi ? v[j] : v[j + 16], keep = hi ? v[j + 16] : v[j];
+            v[j] = keep + dpp_f64<kDppRor8>(send);
+        }
+        c = 16;
+    }
+    {   // xor 4: i - 4 for the upper, i + 4 = i - 12 for the lower
+        const bool hi = (lane & 4) != 0;
+        const int h = c / 2;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (j >= h) break;
+            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
+            const double p4 = dpp_f64<kDppRor4>(send), p12 = dpp_f64<kDppRor12>(send);
+            v[j] = keep + (hi ? p4 : p12);
+        }
+        c = h;
+    }
+    {   // xor 2
+        const bool hi = (lane & 2) != 0;
+        const int h = c / 2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if (j >= h) break;
+            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
+            v[j] = keep + dpp_f64<kDppXor2>(send);
+        }
+        c = h;
+    }
+    {   // xor 1
+        const bool hi = (lane & 1) != 0;
+        const int h = c / 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j >= h) break;
+            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
+            v[j] = keep + dpp_f64<kDppXor1>(send);
+        }
+    }
+}
+// first value index a lane holds after group_reduce_scatter<L>
+template <int L>
+__device__ __forceinline__ int group_rs_base(int lane) {
+    return L == 16 ? 16 * ((lane >> 3) & 1) + 8 * ((lane >> 2) & 1) + 4 * ((lane >> 1) & 1) + 2 * (lane & 1)
+                   : 16 * ((lane >> 2) & 1) + 8 * ((lane >> 1) & 1) + 4 * (lane & 1);
+}
+__device__ __forceinline__ void tri6(int t, int& r, int& s) {   // packed upper index t < 21 -> (r, s), r <= s
+    r = 0;
+    int rem = t;
+    while (rem >= 6 - r) { rem -= 6 - r; ++r; }
+    s = r + rem;
+}
+
+template <int MODEL, bool RATIONAL, bool PRISM, int L>
+__global__ __launch_bounds__(256) void k_edge(LinArgs a) {
+    if (a.state->done) return;
+    constexpr int GPB = 256 / L;   // edges per workgroup
+    const int tid = threadIdx.x, g = tid / L, sub = tid % L;
+    const int e = blockIdx.x * GPB + g;
+    __shared__ double sA[GPB][36], sB[GPB][6], sG[GPB][72], sX[GPB][72];
+    if (e >= a.n_edges) return;   // whole groups: L divides the wave
+    const int4 info = a.edge_info[e];
+    const int cam = info.x, off = info.z, n = info.w;
+    // chain maps (consumed after the sweep): expand the nonzero blocks into Gp, Gg (6 x 6)
+    {
+        const double* ec = a.echain + 54 * (size_t)e;
+        for (int t = sub; t < 72; t += L) {
+            const int w = t / 36, r = (t % 36) / 6, c = t % 6;
+            const double* gb = ec + 27 * w;
+            double v = 0.0;
+            if (r < 3 && c < 3) v = gb[r * 3 + c];
+            else if (r >= 3 && c < 3) v = gb[9 + (r - 3) * 3 + c];
+            else if (r >= 3) v = gb[18 + (r - 3) * 3 + c - 3];
+            sG[g][t] = v;
+        }
+    }
+    double R[9], T[3], kd[12];
+    {
+        const double* er = a.erec + 12 * (size_t)e;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) R[q] = er[q];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) T[q] = er[9 + q];
+    }
+    const float* Kc = a.K + 9 * cam;
+    const double fx = Kc[0], fy = Kc[4], cx = Kc[2], cy = Kc[5], sk = Kc[1];
+    const double xi = MODEL == MCC_MODEL_OMNI ? (double)a.xi[cam] : 0.0;
+    {
+        const int nd = a.nd;
+#pragma unroll
+        for (int q = 0; q < 12; ++q) kd[q] = q < nd ? (double)a.D[nd * cam + q] : 0.0;
+    }
+    double acc[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) acc[q] = 0.0;
+    for (int i = sub; i < n; i += L) {
+        const size_t c = (size_t)off + i;
+        const double X = a.obj_x[c], Y = a.obj_y[c], Z = a.obj_z[c];
+        const float ou = a.img_u[c], ov = a.img_v[c];
+        double Yr[3], D[6];
+        float u, v;
+        if (MODEL == MCC_MODEL_OMNI)
+            omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
+        else
+            pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
+        const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
+        if (a.resid) { a.resid[2 * c] = euf; a.resid[2 * c + 1] = evf; }
+        const double eu = euf, ev = evf;
+        double ju[6], jv[6];   // J' rows: [Y x d, d]
+        ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
+        ju[1] = Yr[2] * D[0] - Yr[0] * D[2];
+        ju[2] = Yr[0] * D[1] - Yr[1] * D[0];
+        ju[3] = D[0]; ju[4] = D[1]; ju[5] = D[2];
+        jv[0] = Yr[1] * D[5] - Yr[2] * D[4];
+        jv[1] = Yr[2] * D[3] - Yr[0] * D[5];
+        jv[2] = Yr[0] * D[4] - Yr[1] * D[3];
+        jv[3] = D[3]; jv[4] = D[4]; jv[5] = D[5];
+        int q = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int s = r; s < 6; ++s) acc[q++] += ju[r] * ju[s] + jv[r] * jv[s];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
+    }
+    group_reduce_scatter<L>(acc, tid);
+    {
+        const int base = group_rs_base<L>(tid);
+#pragma unroll
+        for (int q = 0; q < 32 / L; ++q) {
+            const int idx = base + q;
+            if (idx < 21) {
+                int r, s;
+                tri6(idx, r, s);
+                sA[g][r * 6 + s] = acc[q];
+                sA[g][s * 6 + r] = acc[q];
+            } else if (idx < 27) {
+                sB[g][idx - 21] = acc[q];
+            }
+        }
+    }
+    wave_sync_lds();
+    // X = A' G (A' symmetric)
+    for (int t = sub; t < 72; t += L) {
+        const int w = t / 36, i = (t % 36) / 6, j = t % 6;
+        const double* G = sG[g] + 36 * w;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) s += sA[g][i * 6 + k] * G[k * 6 + j];
+        sX[g][t] = s;
+    }
+    wave_sync_lds();
+    // H = G^T X, g = G^T b':  eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6]
+    double* out = a.eh + 90 * (size_t)e;
+    for (int t = sub; t < 90; t += L) {
+        double s = 0.0;
+        if (t < 42) {
+            const int w = t / 21;
+            int i, j;
+            tri6(t % 21, i, j);
+            const double* Gl = sG[g] + 36 * w;
+            const double* Xr = sX[g] + 36 * w;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s += Gl[k * 6 + i] * Xr[k * 6 + j];
+        } else if (t < 78) {   // Hgp = Gg^T A' Gp: rows global, columns photo
+            const int i = (t - 42) / 6, j = (t - 42) % 6;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s += sG[g][36 + k * 6 + i] * sX[g][k * 6 + j];
+        } else {
+            const int w = (t - 78) / 6, i = (t - 78) % 6;
+            const double* Gl = sG[g] + 36 * w;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s += Gl[k * 6 + i] * sB[g][k];
+        }
+        out[t] = s;
+    }
+}
+
+// One wave per photo vertex: Hpp = sum_e Hpp_e and gp (edge order), the 6 x 6 inverse (register
+// Gauss-Jordan, Hpp SPD), z' = Hpp^-1 gp, Y'_e = Hgp_e Hpp^-1 (-> Y, the next step's photo
+// update), and the photo's Schur pair products at their block-major slots (k_schur).
+__global__ __launch_bounds__(64) void k_photo(LinArgs a) {
+    State* st = a.state;
+    if (st->done) return;
+    const int photo = blockIdx.x, lane = threadIdx.x;
+    const int e0 = a.photo_ptr[photo], ne = a.photo_ptr[photo + 1] - e0;
+    const int pp0 = a.photo_pair_ptr[photo], npp = a.photo_pair_ptr[photo + 1] - pp0;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* sHgp = smem;                 // [ne][36]
+    double* sY = sHgp + 36 * ne;         // [ne][36]
+    double* sHgg = sY + 36 * ne;         // [ne][21]
+    double* sgg = sHgg + 21 * ne;        // [ne][6]
+    double* sHpp = sgg + 6 * ne;         // [36]
+    double* sHi = sHpp + 36;             // [36]
+    double* sgs = sHi + 36;              // [6]
+    int* sgb = reinterpret_cast<int*>(sgs + 6);                                   // [ne]
+    int4* ppl = reinterpret_cast<int4*>(smem + photo_lds_doubles(ne));            // [npp]
+    const double* eh = a.eh + 90 * (size_t)e0;   // the photo's edges are contiguous
+    // sums in edge order: lane t < 21 Hpp upper, 21..26 gp
+    if (lane < 27) {
+        const int col = lane < 21 ? lane : 78 + (lane - 21);
+        double s = 0.0;
+        for (int le = 0; le < ne; ++le) s += eh[90 * le + col];
+        if (lane < 21) {
+            int r, c;
+            tri6(lane, r, c);
+            sHpp[r * 6 + c] = s;
+            sHpp[c * 6 + r] = s;
+        } else {
+            sgs[lane - 21] = s;
+        }
+    }
+    for (int t = lane; t < 36 * ne; t += 64) sHgp[t] = eh[90 * (t / 36) + 42 + t % 36];
+    for (int t = lane; t < 21 * ne; t += 64) sHgg[t] = eh[90 * (t / 21) + 21 + t % 21];
+    for (int t = lane; t < 6 * ne; t += 64) sgg[t] = eh[90 * (t / 6) + 84 + t % 6];
+    for (int t = lane; t < ne; t += 64) sgb[t] = a.gblock[e0 + t];
+    for (int q = lane; q < npp; q += 64) ppl[q] = a.photo_pairs[pp0 + q];
+    wave_sync_lds();
+    {   // register Gauss-Jordan of [Hpp | I]: lane i < 6 owns row i
+        const int li = lane < 6 ? lane : 0;
+        double row[12];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) { row[j] = sHpp[li * 6 + j]; row[6 + j] = li == j ? 1.0 : 0.0; }
+        double dii = 1.0;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double piv = readlane_f64(row[k], k);
+            bad |= !(piv > 0.0);
+            const double pv = piv > 0.0 ? piv : 1.0;
+            double ip = __builtin_amdgcn_rcp(pv);
+            ip = fma(ip, fma(-pv, ip, 1.0), ip);
+            if (lane == k) dii = pv;
+            const double f = lane == k ? 0.0 : row[k] * ip;
+            double pr[12];
+#pragma unroll
+            for (int j = k + 1; j < 12; ++j) pr[j] = readlane_f64(row[j], k);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = k + 1; j < 12; ++j) row[j] -= f * pr[j];
+        }
+        if (lane < 6) {
+            const double id = 1.0 / dii;
+            double zi = 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const double h = row[6 + j] * id;
+                sHi[lane * 6 + j] = h;
+                zi += h * sgs[j];
+            }
+            a.zp[6 * (size_t)photo + lane] = zi;
+            a.gp_tot[6 * (size_t)photo + lane] = sgs[lane];
+        }
+        if (bad && lane == 0) atomicOr(&st->error, 1);
+    }
+    wave_sync_lds();
+    for (int t = lane; t < 36 * ne; t += 64) {   // Y'_e = Hgp_e Hpp^-1
+        const int le = t / 36, ij = t % 36, i = ij / 6, j = ij % 6;
+        double y = 0.0;
+        if (sgb[le] >= 0) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) y += sHgp[36 * le + i * 6 + k] * sHi[k * 6 + j];
+        }
+        sY[t] = y;
+        a.Y[36 * (size_t)e0 + t] = y;
+    }
+    wave_sync_lds();
+    // the photo's Schur pair products at their block-major slots: S_ab entries
+    // ([self] Hgg_a - Y'_a Hgp_b^T), r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
+    for (int t = lane; t < 6 * npp; t += 64) {
+        const int k = t / 6, i = t % 6;
+        const int4 pp = ppl[k];   // {local e1, local e2, self | diagonal block << 1, slot offset}
+        const double* Ya = sY + 36 * pp.x;
+        const double* Hb = sHgp + 36 * pp.y;
+        double y[6];
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) y[kk] = Ya[i * 6 + kk];
+        double* out = a.pairprod + (size_t)pp.w;
+        const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
+        const double* Hgg = sHgg + 21 * pp.x;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double d = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk) d += y[kk] * Hb[j * 6 + kk];
+            double h = 0.0;
+            if (self) {
+                const int r = i < j ? i : j, c = i < j ? j : i;
+                h = Hgg[r * 6 - r * (r - 1) / 2 + (c - r)];
+            }
+            out[i * 6 + j] = self ? h - d : -d;
+        }
+        if (diag) {
+            double d = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < 6; ++kk) d += y[kk] * sgs[kk];
+            out[36 + i] = self ? sgg[6 * pp.x + i] - d : 0.0;
+            out[42 + i] = self ? sgg[6 * pp.x + i] : 0.0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- global solve (one workgroup)
 // Stop test (src/multicalib.cpp:475-477), elimination of the reduced camera system (m <= 128),
 // global-block delta and float32 update.  S (m x m) and r (m) are in LDS and are overwritten.
@@ -2188,6 +2688,41 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     return hipGetLastError();
 }
 
+// split step: lanes per edge of k_edge (88-corner edges: 6 passes at 92% lane use, the 27-value
+// butterfly over 16 lanes is a quarter of a wave's)
+constexpr int kEdgeLanes = 16;
+template <int MODEL, bool RATIONAL, bool PRISM>
+static void launch_edge(const LinArgs& a, hipStream_t s) {
+    constexpr int per = 256 / kEdgeLanes;
+    hipLaunchKernelGGL((k_edge<MODEL, RATIONAL, PRISM, kEdgeLanes>), dim3((a.n_edges + per - 1) / per), dim3(256), 0, s, a);
+}
+size_t mcc_photo_shmem(int max_epp, int max_ppp) {
+    return photo_lds_doubles(max_epp) * sizeof(double) + sizeof(int4) * (size_t)max_ppp;
+}
+hipError_t mcc_launch_split(const LinArgs& a, int model, int max_epp, int max_ppp, bool rational, bool prism,
+                            hipStream_t s) {
+    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
+    const dim3 gp((a.n_photos + 64 / kPrepGroup - 1) / (64 / kPrepGroup));
+    if (model == MCC_MODEL_OMNI) {
+        hipLaunchKernelGGL((k_prep<MCC_MODEL_OMNI>), gp, dim3(64), 0, s, a);
+        launch_edge<MCC_MODEL_OMNI, false, false>(a, s);
+    } else if (model == MCC_MODEL_DOUBLESIDE) {
+        hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE>), gp, dim3(64), 0, s, a);
+        if (rational && prism) launch_edge<MCC_MODEL_DOUBLESIDE, true, true>(a, s);
+        else if (rational) launch_edge<MCC_MODEL_DOUBLESIDE, true, false>(a, s);
+        else if (prism) launch_edge<MCC_MODEL_DOUBLESIDE, false, true>(a, s);
+        else launch_edge<MCC_MODEL_DOUBLESIDE, false, false>(a, s);
+    } else {
+        hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE>), gp, dim3(64), 0, s, a);
+        if (rational && prism) launch_edge<MCC_MODEL_PINHOLE, true, true>(a, s);
+        else if (rational) launch_edge<MCC_MODEL_PINHOLE, true, false>(a, s);
+        else if (prism) launch_edge<MCC_MODEL_PINHOLE, false, true>(a, s);
+        else launch_edge<MCC_MODEL_PINHOLE, false, false>(a, s);
+    }
+    hipLaunchKernelGGL(k_photo, dim3(a.n_photos), dim3(64), mcc_photo_shmem(max_epp, max_ppp), s, a);
+    return hipGetLastError();
+}
+
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
                        (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
@@ -2224,6 +2759,11 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int m
                              SETA(2, true, false, false), SETA(2, false, true, false), SETA(2, true, true, false)})
             if (e != hipSuccess) err = e;
 #undef SETA
+    }
+    const size_t ps = mcc_photo_shmem(max_epp, max_ppp);
+    if (ps > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ps);
+        if (e != hipSuccess) err = e;
     }
     const size_t ss = mcc_solve_shmem(m);
     if (ss > 60 * 1024) {

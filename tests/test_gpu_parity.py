@@ -62,12 +62,31 @@ CASES = {
     "omni_skew": _omni_skew,
     "cams22_m126": lambda: rig.make_config("config3", n_cams=22, n_views=120),   # largest global block, 19 edges/photo
 }
+# the split step (k_prep -> k_edge -> k_photo -> k_schur -> k_solve) runs every m > 30 problem; these
+# force it (MCC_FUSED=0) on the small-m models and distortion variants the fused step otherwise takes
+SPLIT = ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd8_rational", "nd12_prism"]
+for _n in SPLIT:
+    CASES[_n + "_split"] = CASES[_n]
+
+
+def make_adjuster(name, p):
+    if not name.endswith("_split"):
+        return api.BundleAdjuster(p)
+    old = os.environ.get("MCC_FUSED")
+    os.environ["MCC_FUSED"] = "0"
+    try:
+        return api.BundleAdjuster(p)
+    finally:
+        if old is None:
+            del os.environ["MCC_FUSED"]
+        else:
+            os.environ["MCC_FUSED"] = old
 
 
 @pytest.fixture(scope="module", params=sorted(CASES))
 def case(request):
     p = CASES[request.param]()
-    return request.param, p, O.Oracle(p), api.BundleAdjuster(p)
+    return request.param, p, O.Oracle(p), make_adjuster(request.param, p)
 
 
 def test_residuals_bitwise(case):
