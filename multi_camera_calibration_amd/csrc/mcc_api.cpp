@@ -578,6 +578,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->fused = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
     if (const char* f = std::getenv("MCC_FUSED")) p->fused = p->fused && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_SPLIT")) p->split = std::atoi(f) != 0;
+    if (!p->fused && p->split && p->max_epp > 64)
+        return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;
 

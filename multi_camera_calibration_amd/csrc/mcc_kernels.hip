@@ -1494,7 +1494,7 @@ __device__ __forceinline__ void prep_finish(const double* om, const double* Tc, 
 // One edge's prologue (one lane).  gb: the chain maps' nonzero 3x3 blocks, row-major:
 // [0..26]  Gp11, Gp21, Gp22 with Gp = [[Gp11, 0], [Gp21, Gp22]] (photo: J_photo = J' Gp)
 // [27..53] Gg11, Gg21, Gg22 with Gg likewise (camera or double-side block)
-template <int MODEL>
+template <int MODEL, bool BACK>
 __device__ __forceinline__ void prep_edge(const double* R1, const double* Jr1, const double* T1, const double* R2,
                                           const double* Jl2, const double* T2, const double* Rds, const double* Jrds,
                                           const double* dst, int side, double* er, double* gb) {
@@ -1504,7 +1504,7 @@ __device__ __forceinline__ void prep_edge(const double* R1, const double* Jr1, c
     double th3, s3, c3;
     compose(R1, Jr1, T1, R2, Jl2, T2, f, th3, s3, c3);   // compose_motion(photo, camera), :498-500
     double Jl[9], t9[9];
-    if (side == MCC_BACK) {
+    if (BACK && side == MCC_BACK) {
         // compose_motion(ds, photofront), src/mymulticalib.cpp:503-506 / src/doubleSide.cpp:320-322;
         // R(om_front) is the FP64 composed rotation itself (Rodrigues(om_front) to rounding)
         Rot rf0;
@@ -1548,37 +1548,94 @@ __device__ __forceinline__ void prep_edge(const double* R1, const double* Jr1, c
 }
 
 constexpr int kPrepGroup = 16;   // lanes per photo vertex in k_prep (4 photos per wave)
+constexpr int kMaxEdgesPerPhoto = 64;   // split step (k_prep's LDS; mcc_create checks)
+#ifndef MCC_PREP_WAVES
+#define MCC_PREP_WAVES 2           // k_prep waves per SIMD
+#endif
+// camera vertex c's pose (om, T): DoubleSide's fixed cameras, camera 0 = identity, else x
 template <int MODEL>
-__global__ __launch_bounds__(64) void k_prep(LinArgs a) {
+__device__ __forceinline__ void camera_pose(const LinArgs& a, int cam, double* om2, double* T2) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (MODEL == MCC_MODEL_DOUBLESIDE) {
+            om2[k] = a.cam_rt[6 * cam + k];
+            T2[k] = a.cam_rt[6 * cam + 3 + k];
+        } else if (cam == 0) {   // src/mymulticalib.cpp:721-725
+            om2[k] = 0.0;
+            T2[k] = 0.0;
+        } else {
+            om2[k] = a.x[6 * (cam - 1) + k];
+            T2[k] = a.x[6 * (cam - 1) + 3 + k];
+        }
+    }
+}
+// BACK: the problem has back-side edges (MyMulti doubleSideTransform / DoubleSide), so the
+// front-only instantiation carries no second compose
+template <int MODEL, bool BACK>
+__global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     const State* st = a.state;
     if (st->done) return;
     const int tid = threadIdx.x, grp = tid / kPrepGroup, l = tid % kPrepGroup;
     const int photo = blockIdx.x * (64 / kPrepGroup) + grp;
+    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)blockIdx.x + 8 : nullptr;   // MCC_DIAG
+    SSTAMP(stp, 0, 0);
     __shared__ double s_v[64 / kPrepGroup][16];
+    __shared__ double s_part[64 / kPrepGroup][kMaxEdgesPerPhoto][6];
+    __shared__ double s_ph[64 / kPrepGroup][44];   // R1, Jr1, T1, Rds, Jrds, dst (the group's photo)
     const bool valid = photo < a.n_photos;
     const int e0 = valid ? a.photo_ptr[photo] : 0;
     const int ne = valid ? a.photo_ptr[photo + 1] - e0 : 0;
     const int pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
-    // ---- the previous step's photo update, lane k < 6: dp_k = z'_k - sum_e (Y'_e^T dg_g(e))_k in
-    // edge order (k_backsub's photo_delta), G = fl32(alpha dp), x = fl32(x + G)
+    // the camera of the lane's first edge: Rodrigues + Jl, independent of the photo update
+    int4 info0 = make_int4(0, 0, 0, 0);
+    Rot r2;
+    double Jl2[9], T2[3];
+    if (l < ne) {
+        info0 = a.edge_info[e0 + l];
+        double om2[3];
+        camera_pose<MODEL>(a, info0.x, om2, T2);
+        rodrigues_v2m(om2, r2);
+        so3_jac(om2, r2, +1.0, Jl2);
+    }
+    // ---- the previous step's photo update: dp_k = z'_k - sum_e (Y'_e^T dg_g(e))_k in edge order
+    // (k_backsub's photo_delta), G = fl32(alpha dp), x = fl32(x + G).  Lane l forms the 6-vector
+    // Y'_e^T dg of edges l, l + 16, ... (every load of the photo in flight at once), lane k < 6
+    // sums component k over the edges in order.
+    float xo = 0.f;
+    double zk = 0.0;
+    if (valid && l < 6) {
+        xo = xg[l];
+        if (pending) zk = a.zp[6 * (size_t)photo + l];
+    }
+    if (valid && pending) {
+        for (int le = l; le < ne; le += kPrepGroup) {
+            const int g = a.gblock[e0 + le];
+            const double* Ye = a.Y + 36 * (size_t)(e0 + le);
+            double y[36];
+#pragma unroll
+            for (int q = 0; q < 36; ++q) y[q] = Ye[q];
+            const double* d = a.dg + 6 * (g < 0 ? 0 : g);
+            double dv[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) dv[i] = d[i];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                double sk = 0.0;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) sk += y[6 * i + k] * dv[i];
+                s_part[grp][le][k] = g < 0 ? 0.0 : sk;
+            }
+        }
+    }
+    wave_sync_lds();
     double xk = 0.0, Gk = 0.0;
     if (valid && l < 6) {
-        const float xo = xg[l];
         float xn = xo;
         if (pending) {
-            double t = a.zp[6 * (size_t)photo + l];
-            for (int le = 0; le < ne; ++le) {
-                const int g = a.gblock[e0 + le];
-                if (g < 0) continue;
-                const double* Ye = a.Y + 36 * (size_t)(e0 + le) + l;
-                const double* d = a.dg + 6 * g;
-                double s = 0.0;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) s += Ye[6 * i] * d[i];
-                t -= s;
-            }
+            double t = zk;
+            for (int le = 0; le < ne; ++le) t -= s_part[grp][le][l];   // (0 for edges without a global block)
             const float G = (float)(alpha_prev * t);   // G = alpha*delta -> CV_32F (:491-496)
             xn = xo + G;                                // x = x + G (:501)
             xg[l] = xn;
@@ -1591,65 +1648,61 @@ __global__ __launch_bounds__(64) void k_prep(LinArgs a) {
         s_v[grp][8 + l] = Gk;
     }
     wave_sync_lds();
+    SSTAMP(stp, 1, 0);
     if (!valid) return;
-    if (pending && l == 0) {   // ||G||^2, ||x||^2 partials of the applied update (stop test)
-        double g2 = 0.0, x2 = 0.0;
+    double* ph = s_ph[grp];
+    if (l == 0) {   // ||G||^2, ||x||^2 partials of the applied update (stop test); photo Rodrigues
+        if (pending) {
+            double g2 = 0.0, x2 = 0.0;
 #pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            g2 += s_v[grp][8 + q] * s_v[grp][8 + q];
-            x2 += s_v[grp][q] * s_v[grp][q];
+            for (int q = 0; q < 6; ++q) {
+                g2 += s_v[grp][8 + q] * s_v[grp][8 + q];
+                x2 += s_v[grp][q] * s_v[grp][q];
+            }
+            a.photo_norm[2 * (size_t)photo] = g2;
+            a.photo_norm[2 * (size_t)photo + 1] = x2;
         }
-        a.photo_norm[2 * (size_t)photo] = g2;
-        a.photo_norm[2 * (size_t)photo + 1] = x2;
-    }
-    // ---- photo Rodrigues (every lane of the group), the double-side transform
-    const double om1[3] = {s_v[grp][0], s_v[grp][1], s_v[grp][2]};
-    const double T1[3] = {s_v[grp][3], s_v[grp][4], s_v[grp][5]};
-    Rot r1;
-    rodrigues_v2m(om1, r1);
-    double Jr1[9];
-    so3_jac(om1, r1, -1.0, Jr1);
-    double Rds[9], Jrds[9], dst[3];
-    if (a.has_back) {
+        const double om1[3] = {s_v[grp][0], s_v[grp][1], s_v[grp][2]};
+        Rot r1;
+        rodrigues_v2m(om1, r1);
+        so3_jac(om1, r1, -1.0, ph + 9);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) ph[k] = r1.R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ph[18 + k] = s_v[grp][3 + k];
+    } else if (BACK && l == 1) {   // the double-side transform (BACK edges; DoubleSide's global block)
         double dsr[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             dsr[k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[k] : a.ds_rt[k];
-            dst[k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[3 + k] : a.ds_rt[3 + k];
+            ph[39 + k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[3 + k] : a.ds_rt[3 + k];
         }
         Rot rd;
         rodrigues_v2m(dsr, rd);
-        so3_jac(dsr, rd, -1.0, Jrds);
+        so3_jac(dsr, rd, -1.0, ph + 30);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) Rds[k] = rd.R[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) Rds[k] = Jrds[k] = 0.0;
-        dst[0] = dst[1] = dst[2] = 0.0;
+        for (int k = 0; k < 9; ++k) ph[21 + k] = rd.R[k];
     }
+    wave_sync_lds();
+    SSTAMP(stp, 2, 0);
     // ---- one lane per edge
     for (int le = l; le < ne; le += kPrepGroup) {
         const int e = e0 + le;
-        const int4 info = a.edge_info[e];
-        const int cam = info.x;
-        double om2[3], T2[3];
-        if (MODEL == MCC_MODEL_DOUBLESIDE) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * cam + k]; T2[k] = a.cam_rt[6 * cam + 3 + k]; }
-        } else if (cam == 0) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
-        } else {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { om2[k] = a.x[6 * (cam - 1) + k]; T2[k] = a.x[6 * (cam - 1) + 3 + k]; }
+        int4 info = info0;
+        if (le >= kPrepGroup) {   // more than 16 edges: this edge's camera
+            info = a.edge_info[e];
+            double om2[3];
+            camera_pose<MODEL>(a, info.x, om2, T2);
+            rodrigues_v2m(om2, r2);
+            so3_jac(om2, r2, +1.0, Jl2);
         }
-        Rot r2;
-        rodrigues_v2m(om2, r2);
-        double Jl2[9];
-        so3_jac(om2, r2, +1.0, Jl2);
-        prep_edge<MODEL>(r1.R, Jr1, T1, r2.R, Jl2, T2, Rds, Jrds, dst, info.y, a.erec + 12 * (size_t)e,
-                         a.echain + 54 * (size_t)e);
+        prep_edge<MODEL, BACK>(ph, ph + 9, ph + 18, r2.R, Jl2, T2, ph + 21, ph + 30, ph + 39, info.y,
+                               a.erec + 12 * (size_t)e, a.echain + 54 * (size_t)e);
     }
+#ifdef MCC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SSTAMP(stp, 3, 0);
 }
 
 // Reduce-scatter butterfly of 32 per-lane values over a group of L lanes (L = 16 or 8: one DPP
@@ -1715,18 +1768,133 @@ __device__ __forceinline__ void tri6(int t, int& r, int& s) {   // packed upper 
     s = r + rem;
 }
 
+constexpr int kEdgeChunk = 96;    // corners of one edge staged in LDS at a time (k_edge)
+#ifndef MCC_EDGE_WAVES
+#define MCC_EDGE_WAVES 4            // k_edge waves per SIMD (register budget 128 VGPRs)
+#endif
 template <int MODEL, bool RATIONAL, bool PRISM, int L>
-__global__ __launch_bounds__(256) void k_edge(LinArgs a) {
+__global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     if (a.state->done) return;
-    constexpr int GPB = 256 / L;   // edges per workgroup
+    constexpr int GPB = 64 / L;   // edges per workgroup (one wave)
     const int tid = threadIdx.x, g = tid / L, sub = tid % L;
     const int e = blockIdx.x * GPB + g;
-    __shared__ double sA[GPB][36], sB[GPB][6], sG[GPB][72], sX[GPB][72];
+    long long* stp = (a.stamps && (int)(blockIdx.x / 2) < a.n_photos)
+                         ? a.stamps + kStampStride * (size_t)(blockIdx.x / 2) + 16 + 8 * (blockIdx.x & 1) : nullptr;
+    SSTAMP(stp, 0, 0);
+    // LDS per wave: the staged corners, reused after the sweep for the chain (A', b', G, X), and the
+    // edge's pose / camera (8.6 KB: 4 waves per SIMD)
+    struct Chain { double A[36], B[6], G[72], X[72]; };
+    __shared__ __attribute__((aligned(16))) union { float C[GPB][5][kEdgeChunk]; Chain H[GPB]; } sU;
+    __shared__ double sP[GPB][30];
+    auto& sC = sU.C;
     if (e >= a.n_edges) return;   // whole groups: L divides the wave
     const int4 info = a.edge_info[e];
     const int cam = info.x, off = info.z, n = info.w;
-    // chain maps (consumed after the sweep): expand the nonzero blocks into Gp, Gg (6 x 6)
+    // the edge's corners (contiguous in all five streams) -> LDS, every load in flight at once;
+    // chain maps (consumed after the sweep) expanded into Gp, Gg (6 x 6)
+    auto stage = [&](int c0, int cn) {   // every load of the chunk issued before the first LDS store
+        constexpr int PER = kEdgeChunk / L;
+        float v[PER][5];
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = sub + L * u;
+            const size_t c = (size_t)off + c0 + (i < cn ? i : 0);
+            v[u][0] = a.obj_x[c];
+            v[u][1] = a.obj_y[c];
+            v[u][2] = a.obj_z[c];
+            v[u][3] = a.img_u[c];
+            v[u][4] = a.img_v[c];
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = sub + L * u;
+            if (i < cn) {
+#pragma unroll
+                for (int f = 0; f < 5; ++f) sC[g][f][i] = v[u][f];
+            }
+        }
+    };
+    stage(0, min(n, kEdgeChunk));
+    SSTAMP(stp, 1, 0);
+    // the edge's pose and camera (R, T, fx, fy, cx, cy, skew, xi, k[12]) in LDS, re-read by every
+    // corner (an opaque offset keeps the compiler from hoisting them into ~50 more VGPRs, which
+    // would halve the waves per SIMD)
     {
+        double* P = sP[g];
+        const double* er = a.erec + 12 * (size_t)e;
+        const float* Kc = a.K + 9 * cam;
+        const int nd = a.nd;
+        for (int t = sub; t < 30; t += L) {
+            double v;
+            if (t < 12) v = er[t];
+            else if (t < 17) v = (double)Kc[t == 12 ? 0 : t == 13 ? 4 : t == 14 ? 2 : t == 15 ? 5 : 1];
+            else if (t == 17) v = MODEL == MCC_MODEL_OMNI ? (double)a.xi[cam] : 0.0;
+            else v = t - 18 < nd ? (double)a.D[nd * cam + (t - 18)] : 0.0;
+            P[t] = v;
+        }
+    }
+    double acc[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) acc[q] = 0.0;
+    for (int c0 = 0; c0 < n; c0 += kEdgeChunk) {
+        const int cn = min(n - c0, kEdgeChunk);
+        if (c0 > 0) {
+            wave_sync_lds();   // the previous chunk is consumed
+            stage(c0, cn);
+        }
+        wave_sync_lds();
+#pragma unroll 1
+        for (int i = sub; i < cn; i += L) {
+            int po = 0;
+            asm volatile("" : "+v"(po));
+            const double* P = sP[g] + po;
+            double R[9], T[3], kd[12];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) R[q] = P[q];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) T[q] = P[9 + q];
+#pragma unroll
+            for (int q = 0; q < 12; ++q) kd[q] = P[18 + q];
+            const double fx = P[12], fy = P[13], cx = P[14], cy = P[15], sk = P[16], xi = P[17];
+            const double X = sC[g][0][i], Y = sC[g][1][i], Z = sC[g][2][i];
+            const float ou = sC[g][3][i], ov = sC[g][4][i];
+            double Yr[3], D[6];
+            float u, v;
+            if (MODEL == MCC_MODEL_OMNI)
+                omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
+            else
+                pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
+            const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
+            if (a.resid) {
+                const size_t c = (size_t)off + c0 + i;
+                a.resid[2 * c] = euf;
+                a.resid[2 * c + 1] = evf;
+            }
+            const double eu = euf, ev = evf;
+            double ju[6], jv[6];   // J' rows: [Y x d, d]
+            ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
+            ju[1] = Yr[2] * D[0] - Yr[0] * D[2];
+            ju[2] = Yr[0] * D[1] - Yr[1] * D[0];
+            ju[3] = D[0]; ju[4] = D[1]; ju[5] = D[2];
+            jv[0] = Yr[1] * D[5] - Yr[2] * D[4];
+            jv[1] = Yr[2] * D[3] - Yr[0] * D[5];
+            jv[2] = Yr[0] * D[4] - Yr[1] * D[3];
+            jv[3] = D[3]; jv[4] = D[4]; jv[5] = D[5];
+            int q = 0;
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int s2 = r; s2 < 6; ++s2) acc[q++] += ju[r] * ju[s2] + jv[r] * jv[s2];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
+        }
+    }
+    SSTAMP(stp, 2, 0);
+    group_reduce_scatter<L>(acc, tid);
+    wave_sync_lds();   // the corners are consumed: the union's chain view from here on
+    SSTAMP(stp, 3, 0);
+    Chain& CH = sU.H[g];
+    {   // chain maps: the nonzero 3 x 3 blocks -> Gp, Gg (6 x 6)
         const double* ec = a.echain + 54 * (size_t)e;
         for (int t = sub; t < 72; t += L) {
             const int w = t / 36, r = (t % 36) / 6, c = t % 6;
@@ -1735,109 +1903,99 @@ __global__ __launch_bounds__(256) void k_edge(LinArgs a) {
             if (r < 3 && c < 3) v = gb[r * 3 + c];
             else if (r >= 3 && c < 3) v = gb[9 + (r - 3) * 3 + c];
             else if (r >= 3) v = gb[18 + (r - 3) * 3 + c - 3];
-            sG[g][t] = v;
+            CH.G[t] = v;
         }
     }
-    double R[9], T[3], kd[12];
-    {
-        const double* er = a.erec + 12 * (size_t)e;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) R[q] = er[q];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) T[q] = er[9 + q];
-    }
-    const float* Kc = a.K + 9 * cam;
-    const double fx = Kc[0], fy = Kc[4], cx = Kc[2], cy = Kc[5], sk = Kc[1];
-    const double xi = MODEL == MCC_MODEL_OMNI ? (double)a.xi[cam] : 0.0;
-    {
-        const int nd = a.nd;
-#pragma unroll
-        for (int q = 0; q < 12; ++q) kd[q] = q < nd ? (double)a.D[nd * cam + q] : 0.0;
-    }
-    double acc[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) acc[q] = 0.0;
-    for (int i = sub; i < n; i += L) {
-        const size_t c = (size_t)off + i;
-        const double X = a.obj_x[c], Y = a.obj_y[c], Z = a.obj_z[c];
-        const float ou = a.img_u[c], ov = a.img_v[c];
-        double Yr[3], D[6];
-        float u, v;
-        if (MODEL == MCC_MODEL_OMNI)
-            omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
-        else
-            pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
-        const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
-        if (a.resid) { a.resid[2 * c] = euf; a.resid[2 * c + 1] = evf; }
-        const double eu = euf, ev = evf;
-        double ju[6], jv[6];   // J' rows: [Y x d, d]
-        ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
-        ju[1] = Yr[2] * D[0] - Yr[0] * D[2];
-        ju[2] = Yr[0] * D[1] - Yr[1] * D[0];
-        ju[3] = D[0]; ju[4] = D[1]; ju[5] = D[2];
-        jv[0] = Yr[1] * D[5] - Yr[2] * D[4];
-        jv[1] = Yr[2] * D[3] - Yr[0] * D[5];
-        jv[2] = Yr[0] * D[4] - Yr[1] * D[3];
-        jv[3] = D[3]; jv[4] = D[4]; jv[5] = D[5];
-        int q = 0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int s = r; s < 6; ++s) acc[q++] += ju[r] * ju[s] + jv[r] * jv[s];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
-    }
-    group_reduce_scatter<L>(acc, tid);
     {
         const int base = group_rs_base<L>(tid);
 #pragma unroll
         for (int q = 0; q < 32 / L; ++q) {
             const int idx = base + q;
             if (idx < 21) {
-                int r, s;
-                tri6(idx, r, s);
-                sA[g][r * 6 + s] = acc[q];
-                sA[g][s * 6 + r] = acc[q];
+                int r, s2;
+                tri6(idx, r, s2);
+                CH.A[r * 6 + s2] = acc[q];
+                CH.A[s2 * 6 + r] = acc[q];
             } else if (idx < 27) {
-                sB[g][idx - 21] = acc[q];
+                CH.B[idx - 21] = acc[q];
             }
         }
     }
     wave_sync_lds();
-    // X = A' G (A' symmetric)
-    for (int t = sub; t < 72; t += L) {
-        const int w = t / 36, i = (t % 36) / 6, j = t % 6;
-        const double* G = sG[g] + 36 * w;
-        double s = 0.0;
+    // X = A' G (A' symmetric): lane (w, i) < 12 forms row i of X_w, its operands (A' row i, all of
+    // G_w) read at once (16-B LDS reads: one round trip)
+    if (sub < 12) {
+        const int w = sub / 6, i = sub % 6;
+        double ar[6], gm[36], xr[6];
+        const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
+        const double2* G2 = reinterpret_cast<const double2*>(CH.G + 36 * w);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) s += sA[g][i * 6 + k] * G[k * 6 + j];
-        sX[g][t] = s;
+        for (int q = 0; q < 3; ++q) { const double2 v = A2[q]; ar[2 * q] = v.x; ar[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < 18; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s2 += ar[k] * gm[k * 6 + j];
+            xr[j] = s2;
+        }
+        double2* X2 = reinterpret_cast<double2*>(CH.X + 36 * w + 6 * i);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
     }
     wave_sync_lds();
-    // H = G^T X, g = G^T b':  eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6]
+    // H = G^T X, g = G^T b':  eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Tasks:
+    // rows i of Hpp (Gp, Xp), Hgg (Gg, Xg), Hgp (Gg, Xp: rows global, columns photo), then gp, gg
     double* out = a.eh + 90 * (size_t)e;
-    for (int t = sub; t < 90; t += L) {
-        double s = 0.0;
-        if (t < 42) {
-            const int w = t / 21;
-            int i, j;
-            tri6(t % 21, i, j);
-            const double* Gl = sG[g] + 36 * w;
-            const double* Xr = sX[g] + 36 * w;
+    for (int task = sub; task < 20; task += L) {
+        if (task < 18) {
+            const int blk = task / 6, i = task % 6;
+            const double* Gl = CH.G + (blk == 0 ? 0 : 36);
+            const double2* X2 = reinterpret_cast<const double2*>(CH.X + (blk == 1 ? 36 : 0));
+            double gc[6], xm[36];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) s += Gl[k * 6 + i] * Xr[k * 6 + j];
-        } else if (t < 78) {   // Hgp = Gg^T A' Gp: rows global, columns photo
-            const int i = (t - 42) / 6, j = (t - 42) % 6;
+            for (int k = 0; k < 6; ++k) gc[k] = Gl[k * 6 + i];   // column i of G
 #pragma unroll
-            for (int k = 0; k < 6; ++k) s += sG[g][36 + k * 6 + i] * sX[g][k * 6 + j];
+            for (int q = 0; q < 18; ++q) { const double2 v = X2[q]; xm[2 * q] = v.x; xm[2 * q + 1] = v.y; }
+            double h[6];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double s2 = 0.0;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) s2 += gc[k] * xm[k * 6 + j];
+                h[j] = s2;
+            }
+            if (blk < 2) {   // upper row i: packed at 21 blk + 6 i - i (i - 1) / 2, columns j >= i
+                double* o = out + 21 * blk + 6 * i - i * (i - 1) / 2 - i;
+#pragma unroll
+                for (int j = 0; j < 6; ++j)
+                    if (j >= i) o[j] = h[j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) out[42 + 6 * i + j] = h[j];
+            }
         } else {
-            const int w = (t - 78) / 6, i = (t - 78) % 6;
-            const double* Gl = sG[g] + 36 * w;
+            const int w = task - 18;
+            const double2* G2 = reinterpret_cast<const double2*>(CH.G + 36 * w);
+            double gm[36], b[6];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) s += Gl[k * 6 + i] * sB[g][k];
+            for (int q = 0; q < 18; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) b[k] = CH.B[k];
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double s2 = 0.0;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) s2 += gm[k * 6 + j] * b[k];
+                out[78 + 6 * w + j] = s2;
+            }
         }
-        out[t] = s;
     }
+#ifdef MCC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SSTAMP(stp, 4, 0);
 }
 
 // One wave per photo vertex: Hpp = sum_e Hpp_e and gp (edge order), the 6 x 6 inverse (register
@@ -1847,24 +2005,53 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
     State* st = a.state;
     if (st->done) return;
     const int photo = blockIdx.x, lane = threadIdx.x;
+    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)photo : nullptr;   // MCC_DIAG: slots 0..7
+    SSTAMP(stp, 0, 0);
     const int e0 = a.photo_ptr[photo], ne = a.photo_ptr[photo + 1] - e0;
     const int pp0 = a.photo_pair_ptr[photo], npp = a.photo_pair_ptr[photo + 1] - pp0;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* sHgp = smem;                 // [ne][36]
-    double* sY = sHgp + 36 * ne;         // [ne][36]
-    double* sHgg = sY + 36 * ne;         // [ne][21]
-    double* sgg = sHgg + 21 * ne;        // [ne][6]
-    double* sHpp = sgg + 6 * ne;         // [36]
+    double* sE = smem;                   // [ne][90]: the edges' eh records
+    double* sY = sE + 90 * ne;           // [ne][36]
+    double* sHpp = sY + 36 * ne;         // [36]
     double* sHi = sHpp + 36;             // [36]
     double* sgs = sHi + 36;              // [6]
     int* sgb = reinterpret_cast<int*>(sgs + 6);                                   // [ne]
     int4* ppl = reinterpret_cast<int4*>(smem + photo_lds_doubles(ne));            // [npp]
-    const double* eh = a.eh + 90 * (size_t)e0;   // the photo's edges are contiguous
+    // the photo's edges are contiguous: its eh block (90 ne doubles), gblocks and Schur pairs ->
+    // LDS, eight loads per lane in flight per round
+    {
+        constexpr int U = 24;   // 24 x 64 doubles per round: one round up to 17 edges
+        const int4 pq0 = lane < npp ? a.photo_pairs[pp0 + lane] : make_int4(0, 0, 0, 0);
+        const int4 pq1 = lane + 64 < npp ? a.photo_pairs[pp0 + lane + 64] : make_int4(0, 0, 0, 0);
+        const int gbv = lane < ne ? a.gblock[e0 + lane] : -1;
+        const double* src = a.eh + 90 * (size_t)e0;
+        const int tot = 90 * ne;
+        for (int t0 = 0; t0 < tot; t0 += 64 * U) {
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = t0 + lane + 64 * u;
+                v[u] = src[t < tot ? t : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = t0 + lane + 64 * u;
+                if (t < tot) sE[t] = v[u];
+            }
+        }
+        if (lane < ne) sgb[lane] = gbv;
+        for (int t = lane + 64; t < ne; t += 64) sgb[t] = a.gblock[e0 + t];
+        if (lane < npp) ppl[lane] = pq0;
+        if (lane + 64 < npp) ppl[lane + 64] = pq1;
+        for (int q = lane + 128; q < npp; q += 64) ppl[q] = a.photo_pairs[pp0 + q];
+    }
+    wave_sync_lds();
+    SSTAMP(stp, 1, 0);
     // sums in edge order: lane t < 21 Hpp upper, 21..26 gp
     if (lane < 27) {
         const int col = lane < 21 ? lane : 78 + (lane - 21);
         double s = 0.0;
-        for (int le = 0; le < ne; ++le) s += eh[90 * le + col];
+        for (int le = 0; le < ne; ++le) s += sE[90 * le + col];
         if (lane < 21) {
             int r, c;
             tri6(lane, r, c);
@@ -1874,12 +2061,8 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
             sgs[lane - 21] = s;
         }
     }
-    for (int t = lane; t < 36 * ne; t += 64) sHgp[t] = eh[90 * (t / 36) + 42 + t % 36];
-    for (int t = lane; t < 21 * ne; t += 64) sHgg[t] = eh[90 * (t / 21) + 21 + t % 21];
-    for (int t = lane; t < 6 * ne; t += 64) sgg[t] = eh[90 * (t / 6) + 84 + t % 6];
-    for (int t = lane; t < ne; t += 64) sgb[t] = a.gblock[e0 + t];
-    for (int q = lane; q < npp; q += 64) ppl[q] = a.photo_pairs[pp0 + q];
     wave_sync_lds();
+    SSTAMP(stp, 2, 0);
     {   // register Gauss-Jordan of [Hpp | I]: lane i < 6 owns row i
         const int li = lane < 6 ? lane : 0;
         double row[12];
@@ -1918,30 +2101,51 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
         if (bad && lane == 0) atomicOr(&st->error, 1);
     }
     wave_sync_lds();
-    for (int t = lane; t < 36 * ne; t += 64) {   // Y'_e = Hgp_e Hpp^-1
-        const int le = t / 36, ij = t % 36, i = ij / 6, j = ij % 6;
-        double y = 0.0;
-        if (sgb[le] >= 0) {
+    SSTAMP(stp, 3, 0);
+    for (int t = lane; t < 6 * ne; t += 64) {   // Y'_e = Hgp_e Hpp^-1: task (edge, row i)
+        const int le = t / 6, i = t % 6;
+        double hr[6], hi[36], y[6];
+        const double2* H2 = reinterpret_cast<const double2*>(sE + 90 * le + 42 + 6 * i);
+        const double2* I2 = reinterpret_cast<const double2*>(sHi);
 #pragma unroll
-            for (int k = 0; k < 6; ++k) y += sHgp[36 * le + i * 6 + k] * sHi[k * 6 + j];
+        for (int q = 0; q < 3; ++q) { const double2 v = H2[q]; hr[2 * q] = v.x; hr[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < 18; ++q) { const double2 v = I2[q]; hi[2 * q] = v.x; hi[2 * q + 1] = v.y; }
+        const bool gl = sgb[le] >= 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double v = 0.0;
+            if (gl) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) v += hr[k] * hi[k * 6 + j];
+            }
+            y[j] = v;
         }
-        sY[t] = y;
-        a.Y[36 * (size_t)e0 + t] = y;
+        double2* Y2 = reinterpret_cast<double2*>(sY + 36 * le + 6 * i);
+        double2* G2 = reinterpret_cast<double2*>(a.Y + 36 * (size_t)(e0 + le) + 6 * i);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            Y2[q] = make_double2(y[2 * q], y[2 * q + 1]);
+            G2[q] = make_double2(y[2 * q], y[2 * q + 1]);
+        }
     }
     wave_sync_lds();
+    SSTAMP(stp, 4, 0);
     // the photo's Schur pair products at their block-major slots: S_ab entries
     // ([self] Hgg_a - Y'_a Hgp_b^T), r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
     for (int t = lane; t < 6 * npp; t += 64) {
         const int k = t / 6, i = t % 6;
         const int4 pp = ppl[k];   // {local e1, local e2, self | diagonal block << 1, slot offset}
-        const double* Ya = sY + 36 * pp.x;
-        const double* Hb = sHgp + 36 * pp.y;
-        double y[6];
+        const double2* Y2 = reinterpret_cast<const double2*>(sY + 36 * pp.x + 6 * i);
+        const double2* B2 = reinterpret_cast<const double2*>(sE + 90 * pp.y + 42);
+        double y[6], Hb[36];
 #pragma unroll
-        for (int kk = 0; kk < 6; ++kk) y[kk] = Ya[i * 6 + kk];
+        for (int q = 0; q < 3; ++q) { const double2 v = Y2[q]; y[2 * q] = v.x; y[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < 18; ++q) { const double2 v = B2[q]; Hb[2 * q] = v.x; Hb[2 * q + 1] = v.y; }
         double* out = a.pairprod + (size_t)pp.w;
         const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
-        const double* Hgg = sHgg + 21 * pp.x;
+        const double* Hgg = sE + 90 * pp.x + 21;
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             double d = 0.0;
@@ -1952,16 +2156,25 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
                 const int r = i < j ? i : j, c = i < j ? j : i;
                 h = Hgg[r * 6 - r * (r - 1) / 2 + (c - r)];
             }
+#ifndef MCC_EXP_NO_PAIRSTORE
             out[i * 6 + j] = self ? h - d : -d;
+#else
+            if (d == 12345.0) out[i * 6 + j] = self ? h - d : -d;
+#endif
         }
         if (diag) {
             double d = 0.0;
 #pragma unroll
             for (int kk = 0; kk < 6; ++kk) d += y[kk] * sgs[kk];
-            out[36 + i] = self ? sgg[6 * pp.x + i] - d : 0.0;
-            out[42 + i] = self ? sgg[6 * pp.x + i] : 0.0;
+            const double gg = sE[90 * pp.x + 84 + i];
+            out[36 + i] = self ? gg - d : 0.0;
+            out[42 + i] = self ? gg : 0.0;
         }
     }
+#ifdef MCC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SSTAMP(stp, 5, 0);
 }
 
 // ---------------------------------------------------------------- global solve (one workgroup)
@@ -2331,16 +2544,20 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             // the products k_linearize wrote at the block's slots: independent coalesced loads,
             // eight in flight per thread (entries >= 36 of an off-diagonal block: none, zeros)
             if (q < sz) {
+                // slots sub, sub + kSub, ... summed in that order; 24 loads per thread in flight per
+                // round (one round for the ~100-slot items of a 5k-view rig)
                 const double* pp = a.pairprod + (size_t)it.y + q;
-                int p = sub;
-                for (; p + 7 * kSub < it.z; p += 8 * kSub) {
-                    double v[8];
+                constexpr int U = 24;
+                for (int p0 = sub; p0 < it.z; p0 += U * kSub) {
+                    double v[U];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = pp[(size_t)sz * (p + u * kSub)];
+                    for (int u = 0; u < U; ++u) {
+                        const int p = p0 + u * kSub;
+                        v[u] = p < it.z ? pp[(size_t)sz * p] : 0.0;
+                    }
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) s += v[u];
+                    for (int u = 0; u < U; ++u) s += v[u];
                 }
-                for (; p < it.z; p += kSub) s += pp[(size_t)sz * p];
             }
             part[sub][q] = s;
         }
@@ -2693,8 +2910,8 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
 constexpr int kEdgeLanes = 16;
 template <int MODEL, bool RATIONAL, bool PRISM>
 static void launch_edge(const LinArgs& a, hipStream_t s) {
-    constexpr int per = 256 / kEdgeLanes;
-    hipLaunchKernelGGL((k_edge<MODEL, RATIONAL, PRISM, kEdgeLanes>), dim3((a.n_edges + per - 1) / per), dim3(256), 0, s, a);
+    constexpr int per = 64 / kEdgeLanes;
+    hipLaunchKernelGGL((k_edge<MODEL, RATIONAL, PRISM, kEdgeLanes>), dim3((a.n_edges + per - 1) / per), dim3(64), 0, s, a);
 }
 size_t mcc_photo_shmem(int max_epp, int max_ppp) {
     return photo_lds_doubles(max_epp) * sizeof(double) + sizeof(int4) * (size_t)max_ppp;
@@ -2704,16 +2921,17 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, int max_epp, int max_pp
     if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
     const dim3 gp((a.n_photos + 64 / kPrepGroup - 1) / (64 / kPrepGroup));
     if (model == MCC_MODEL_OMNI) {
-        hipLaunchKernelGGL((k_prep<MCC_MODEL_OMNI>), gp, dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_prep<MCC_MODEL_OMNI, false>), gp, dim3(64), 0, s, a);
         launch_edge<MCC_MODEL_OMNI, false, false>(a, s);
     } else if (model == MCC_MODEL_DOUBLESIDE) {
-        hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE>), gp, dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE, true>), gp, dim3(64), 0, s, a);
         if (rational && prism) launch_edge<MCC_MODEL_DOUBLESIDE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_DOUBLESIDE, true, false>(a, s);
         else if (prism) launch_edge<MCC_MODEL_DOUBLESIDE, false, true>(a, s);
         else launch_edge<MCC_MODEL_DOUBLESIDE, false, false>(a, s);
     } else {
-        hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE>), gp, dim3(64), 0, s, a);
+        if (a.has_back) hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, true>), gp, dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, false>), gp, dim3(64), 0, s, a);
         if (rational && prism) launch_edge<MCC_MODEL_PINHOLE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_PINHOLE, true, false>(a, s);
         else if (prism) launch_edge<MCC_MODEL_PINHOLE, false, true>(a, s);
