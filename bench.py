@@ -159,11 +159,18 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
                 ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)})
 
 
-def roofline(st, lin_ms, tr=None):
+def lin_kernels(p) -> str:
+    """The kernels of the linearisation window (mcc_timing_*): one fused kernel for m <= 30, the
+    split step's three for m > 30."""
+    m = 6 if p.model == rig.DOUBLESIDE else 6 * (p.n_cams - 1)
+    return "k_prep+k_edge+k_photo" if m > 30 else "k_linearize"
+
+
+def roofline(st, lin_ms, tr=None, kernel="k_linearize"):
     achieved = st["alg_bytes"] / (lin_ms * 1e-3) / 1e9
     return {
         "bound": "hbm",
-        "kernel": "k_linearize",
+        "kernel": kernel,
         "achieved": achieved,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -192,7 +199,7 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
            "model": {rig.PINHOLE: "pinhole", rig.OMNI: "omnidir", rig.DOUBLESIDE: "doubleside"}[p.model],
            "steps": steps, "ms_per_step": ms, "corner_evals_per_s": p.n_corners / (ms * 1e-3),
            "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
-           "roofline": roofline(st, m["lin_ms"]), "rig_generation_s": round(gen_s, 2)}
+           "roofline": roofline(st, m["lin_ms"], kernel=lin_kernels(p)), "rig_generation_s": round(gen_s, 2)}
     fp = load_profile("fp64", name, p.n_photos)
     if fp and fp.get("fp64_flops_per_launch"):
         tf = fp["fp64_flops_per_launch"] / (m["lin_ms"] * 1e-3) / 1e12
@@ -310,7 +317,7 @@ def main():
     if rank != 0:
         return
     tr = load_profile("traffic", args.config, views_per_rank) if world == 1 else None
-    rl = roofline(st, m["lin_ms"], tr)
+    rl = roofline(st, m["lin_ms"], tr, kernel=lin_kernels(prob))
     rl["kernel_launches_timed"] = m["nlaunch"]
     rl["step_ms_events"] = m["step_ms_ev"]
     out = {

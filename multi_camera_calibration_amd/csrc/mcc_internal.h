@@ -95,10 +95,10 @@ struct LinArgs {
     double* eh;              // [90E] Hpp upper (21), Hgg upper (21), Hgp (36), gp (6), gg (6) (k_edge -> k_photo)
 };
 
-// k_photo's LDS: the edges' eh records [ne][90], Y' [ne][36], Hpp, Hpp^-1 [36], gp [6], gblock
-// [ne] ints, then (16-B aligned) the photo's Schur pairs
+// k_photo's LDS: per edge [Hgg upper 21 | pad | U 36 | gg 6] (64 doubles), the Hpp / gp sums [28],
+// Hpp's inverse Cholesky factor [36], v [6], gblock [ne] ints, then (16-B aligned) the Schur pairs
 __host__ __device__ inline size_t photo_lds_doubles(int ne) {
-    return ((size_t)126 * ne + 78 + (size_t)(ne + 1) / 2 + 1) & ~(size_t)1;
+    return ((size_t)64 * ne + 70 + (size_t)(ne + 1) / 2 + 1) & ~(size_t)1;
 }
 
 struct SchurArgs {

@@ -1795,10 +1795,14 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     auto stage = [&](int c0, int cn) {   // every load of the chunk issued before the first LDS store
         constexpr int PER = kEdgeChunk / L;
         float v[PER][5];
+        int sb = sub;   // opaque: the lane's chunk offsets are recomputed per chunk, not kept live (spilled)
+        asm volatile("" : "+v"(sb));
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int i = sub + L * u;
-            const size_t c = (size_t)off + c0 + (i < cn ? i : 0);
+            const int i = sb + L * u;
+            // 32-bit element index: SGPR base + one VGPR offset per load (saddr form), not a 64-bit
+            // address pair per stream, which spilled to scratch
+            const unsigned c = (unsigned)(off + c0 + (i < cn ? i : 0));
             v[u][0] = a.obj_x[c];
             v[u][1] = a.obj_y[c];
             v[u][2] = a.obj_z[c];
@@ -1807,7 +1811,7 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int i = sub + L * u;
+            const int i = sb + L * u;
             if (i < cn) {
 #pragma unroll
                 for (int f = 0; f < 5; ++f) sC[g][f][i] = v[u][f];
@@ -1890,13 +1894,19 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
         }
     }
     SSTAMP(stp, 2, 0);
-    group_reduce_scatter<L>(acc, tid);
+    // after the sweep: lane indices re-derived from one opaque copy of the thread id, so that only it
+    // (not e, g, sub and their addresses) stays live through the sweep at 128 VGPRs
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
+    const int gq = tq / L, sq = tq % L;
+    const int eq = blockIdx.x * GPB + gq;
+    group_reduce_scatter<L>(acc, tq);
     wave_sync_lds();   // the corners are consumed: the union's chain view from here on
     SSTAMP(stp, 3, 0);
-    Chain& CH = sU.H[g];
+    Chain& CH = sU.H[gq];
     {   // chain maps: the nonzero 3 x 3 blocks -> Gp, Gg (6 x 6)
-        const double* ec = a.echain + 54 * (size_t)e;
-        for (int t = sub; t < 72; t += L) {
+        const double* ec = a.echain + 54 * (size_t)eq;
+        for (int t = sq; t < 72; t += L) {
             const int w = t / 36, r = (t % 36) / 6, c = t % 6;
             const double* gb = ec + 27 * w;
             double v = 0.0;
@@ -1907,7 +1917,7 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
         }
     }
     {
-        const int base = group_rs_base<L>(tid);
+        const int base = group_rs_base<L>(tq);
 #pragma unroll
         for (int q = 0; q < 32 / L; ++q) {
             const int idx = base + q;
@@ -1924,8 +1934,8 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     wave_sync_lds();
     // X = A' G (A' symmetric): lane (w, i) < 12 forms row i of X_w, its operands (A' row i, all of
     // G_w) read at once (16-B LDS reads: one round trip)
-    if (sub < 12) {
-        const int w = sub / 6, i = sub % 6;
+    if (sq < 12) {
+        const int w = sq / 6, i = sq % 6;
         double ar[6], gm[36], xr[6];
         const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
         const double2* G2 = reinterpret_cast<const double2*>(CH.G + 36 * w);
@@ -1947,8 +1957,8 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     wave_sync_lds();
     // H = G^T X, g = G^T b':  eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Tasks:
     // rows i of Hpp (Gp, Xp), Hgg (Gg, Xg), Hgp (Gg, Xp: rows global, columns photo), then gp, gg
-    double* out = a.eh + 90 * (size_t)e;
-    for (int task = sub; task < 20; task += L) {
+    double* out = a.eh + 90 * (size_t)eq;
+    for (int task = sq; task < 20; task += L) {
         if (task < 18) {
             const int blk = task / 6, i = task % 6;
             const double* Gl = CH.G + (blk == 0 ? 0 : 36);
@@ -1998,9 +2008,11 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     SSTAMP(stp, 4, 0);
 }
 
-// One wave per photo vertex: Hpp = sum_e Hpp_e and gp (edge order), the 6 x 6 inverse (register
-// Gauss-Jordan, Hpp SPD), z' = Hpp^-1 gp, Y'_e = Hgp_e Hpp^-1 (-> Y, the next step's photo
-// update), and the photo's Schur pair products at their block-major slots (k_schur).
+// One wave per photo vertex: Hpp = sum_e Hpp_e and gp (edge order), its Cholesky factor Hpp = L L^T
+// and Li = L^-1 (so Hpp^-1 = Li^T Li), z' = Hpp^-1 gp, per edge U_e = Hgp_e Li^T (in place of Hgp)
+// and Y'_e = Hgp_e Hpp^-1 = U_e Li (-> Y, the next step's photo update), and the photo's Schur pair
+// products Y'_a Hgp_b^T = U_a U_b^T at their block-major slots (k_schur).  Keeping U instead of both
+// Y' and Hgp halves the LDS per edge (64 doubles), so more photos' chains overlap per CU.
 __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
     State* st = a.state;
     if (st->done) return;
@@ -2010,28 +2022,35 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
     const int e0 = a.photo_ptr[photo], ne = a.photo_ptr[photo + 1] - e0;
     const int pp0 = a.photo_pair_ptr[photo], npp = a.photo_pair_ptr[photo + 1] - pp0;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* sE = smem;                   // [ne][90]: the edges' eh records
-    double* sY = sE + 90 * ne;           // [ne][36]
-    double* sHpp = sY + 36 * ne;         // [36]
-    double* sHi = sHpp + 36;             // [36]
-    double* sgs = sHi + 36;              // [6]
-    int* sgb = reinterpret_cast<int*>(sgs + 6);                                   // [ne]
+    constexpr int ES = 64;               // per edge: Hgg upper [0, 21), pad, U [22, 58), gg [58, 64)
+    double* sE = smem;                   // [ne][ES]
+    double* s27 = sE + ES * ne;          // [28]: Hpp upper 21, gp 6
+    double* sLi = s27 + 28;              // [36]: Li = L^-1 (lower, zeros above)
+    double* sv = sLi + 36;               // [6]:  v = Li gp
+    int* sgb = reinterpret_cast<int*>(sv + 6);                                    // [ne]
     int4* ppl = reinterpret_cast<int4*>(smem + photo_lds_doubles(ne));            // [npp]
-    // the photo's edges are contiguous: its eh block (90 ne doubles), gblocks and Schur pairs ->
-    // LDS, eight loads per lane in flight per round
+    const double* src = a.eh + 90 * (size_t)e0;   // eh = [Hpp 21 | Hgg 21 | Hgp 36 | gp 6 | gg 6]
     {
-        constexpr int U = 24;   // 24 x 64 doubles per round: one round up to 17 edges
+        // lanes < 27: the Hpp / gp column sums in edge order, loaded straight to registers (the
+        // first 16 edges' loads issued before the staging's); every lane: the rest of eh -> LDS
+        constexpr int SB = 16;
+        const bool sl = lane < 27;
+        const int col = lane < 21 ? lane : 78 + (lane - 21);
+        double sv0[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) sv0[u] = (sl && u < ne) ? src[90 * u + col] : 0.0;
         const int4 pq0 = lane < npp ? a.photo_pairs[pp0 + lane] : make_int4(0, 0, 0, 0);
         const int4 pq1 = lane + 64 < npp ? a.photo_pairs[pp0 + lane + 64] : make_int4(0, 0, 0, 0);
         const int gbv = lane < ne ? a.gblock[e0 + lane] : -1;
-        const double* src = a.eh + 90 * (size_t)e0;
-        const int tot = 90 * ne;
+        constexpr int U = 16;
+        const int tot = ES * ne;
         for (int t0 = 0; t0 < tot; t0 += 64 * U) {
             double v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int t = t0 + lane + 64 * u;
-                v[u] = src[t < tot ? t : 0];
+                const int t = t0 + lane + 64 * u, le = t >> 6, c = t & 63;
+                const int sc = c < 21 ? c + 21 : (c < 58 ? c + 20 : c + 26);
+                v[u] = src[t < tot ? 90 * le + sc : 0];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -2039,6 +2058,12 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
                 if (t < tot) sE[t] = v[u];
             }
         }
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < SB; ++u) s += sv0[u];
+        if (sl)
+            for (int le = SB; le < ne; ++le) s += src[90 * le + col];
+        if (sl) s27[lane] = s;
         if (lane < ne) sgb[lane] = gbv;
         for (int t = lane + 64; t < ne; t += 64) sgb[t] = a.gblock[e0 + t];
         if (lane < npp) ppl[lane] = pq0;
@@ -2047,97 +2072,110 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
     }
     wave_sync_lds();
     SSTAMP(stp, 1, 0);
-    // sums in edge order: lane t < 21 Hpp upper, 21..26 gp
-    if (lane < 27) {
-        const int col = lane < 21 ? lane : 78 + (lane - 21);
-        double s = 0.0;
-        for (int le = 0; le < ne; ++le) s += sE[90 * le + col];
-        if (lane < 21) {
-            int r, c;
-            tri6(lane, r, c);
-            sHpp[r * 6 + c] = s;
-            sHpp[c * 6 + r] = s;
-        } else {
-            sgs[lane - 21] = s;
-        }
-    }
-    wave_sync_lds();
-    SSTAMP(stp, 2, 0);
-    {   // register Gauss-Jordan of [Hpp | I]: lane i < 6 owns row i
-        const int li = lane < 6 ? lane : 0;
-        double row[12];
+    if (lane == 0) {   // Cholesky Hpp = L L^T, Li = L^-1, v = Li gp, z' = Li^T v (registers, one lane)
+        double A[21], gs[6], Lm[6][6], Li[6][6];
+        const double2* S2 = reinterpret_cast<const double2*>(s27);
 #pragma unroll
-        for (int j = 0; j < 6; ++j) { row[j] = sHpp[li * 6 + j]; row[6 + j] = li == j ? 1.0 : 0.0; }
-        double dii = 1.0;
+        for (int q = 0; q < 14; ++q) {
+            const double2 w = S2[q];
+            if (2 * q < 21) A[2 * q] = w.x; else gs[2 * q - 21] = w.x;
+            if (2 * q + 1 < 21) A[2 * q + 1] = w.y; else if (2 * q + 1 < 27) gs[2 * q + 1 - 21] = w.y;
+        }
         bool bad = false;
+        double idg[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const double piv = readlane_f64(row[k], k);
-            bad |= !(piv > 0.0);
-            const double pv = piv > 0.0 ? piv : 1.0;
-            double ip = __builtin_amdgcn_rcp(pv);
-            ip = fma(ip, fma(-pv, ip, 1.0), ip);
-            if (lane == k) dii = pv;
-            const double f = lane == k ? 0.0 : row[k] * ip;
-            double pr[12];
+        for (int j = 0; j < 6; ++j) {
+            double d = A[6 * j - j * (j - 1) / 2];
 #pragma unroll
-            for (int j = k + 1; j < 12; ++j) pr[j] = readlane_f64(row[j], k);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int k = 0; k < j; ++k) d -= Lm[j][k] * Lm[j][k];
+            bad |= !(d > 0.0);
+            const double sd = sqrt(d > 0.0 ? d : 1.0);
+            const double is = 1.0 / sd;
+            Lm[j][j] = sd;
+            idg[j] = is;
 #pragma unroll
-            for (int j = k + 1; j < 12; ++j) row[j] -= f * pr[j];
-        }
-        if (lane < 6) {
-            const double id = 1.0 / dii;
-            double zi = 0.0;
+            for (int i = j + 1; i < 6; ++i) {
+                double t = A[6 * j - j * (j - 1) / 2 + (i - j)];   // Hpp(j, i) = Hpp(i, j)
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                const double h = row[6 + j] * id;
-                sHi[lane * 6 + j] = h;
-                zi += h * sgs[j];
+                for (int k = 0; k < j; ++k) t -= Lm[i][k] * Lm[j][k];
+                Lm[i][j] = t * is;
             }
-            a.zp[6 * (size_t)photo + lane] = zi;
-            a.gp_tot[6 * (size_t)photo + lane] = sgs[lane];
         }
-        if (bad && lane == 0) atomicOr(&st->error, 1);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {   // column j of Li: forward substitution of L x = e_j
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (i < j) { Li[i][j] = 0.0; continue; }
+                double t = i == j ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = j; k < i; ++k) t -= Lm[i][k] * Li[k][j];
+                Li[i][j] = t * idg[i];
+            }
+        }
+        double v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k <= i; ++k) t += Li[i][k] * gs[k];
+            v[i] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double t = 0.0;
+#pragma unroll
+            for (int i = j; i < 6; ++i) t += Li[i][j] * v[i];
+            a.zp[6 * (size_t)photo + j] = t;
+            a.gp_tot[6 * (size_t)photo + j] = gs[j];
+            sv[j] = v[j];
+        }
+        double2* L2 = reinterpret_cast<double2*>(sLi);
+#pragma unroll
+        for (int q = 0; q < 18; ++q) L2[q] = make_double2(Li[(2 * q) / 6][(2 * q) % 6], Li[(2 * q + 1) / 6][(2 * q + 1) % 6]);
+        if (bad) atomicOr(&st->error, 1);
     }
     wave_sync_lds();
     SSTAMP(stp, 3, 0);
-    for (int t = lane; t < 6 * ne; t += 64) {   // Y'_e = Hgp_e Hpp^-1: task (edge, row i)
+    for (int t = lane; t < 6 * ne; t += 64) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
         const int le = t / 6, i = t % 6;
-        double hr[6], hi[36], y[6];
-        const double2* H2 = reinterpret_cast<const double2*>(sE + 90 * le + 42 + 6 * i);
-        const double2* I2 = reinterpret_cast<const double2*>(sHi);
+        double h[6], li[36], u[6], y[6];
+        double2* H2 = reinterpret_cast<double2*>(sE + ES * le + 22 + 6 * i);
+        const double2* I2 = reinterpret_cast<const double2*>(sLi);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) { const double2 v = H2[q]; hr[2 * q] = v.x; hr[2 * q + 1] = v.y; }
+        for (int q = 0; q < 3; ++q) { const double2 w = H2[q]; h[2 * q] = w.x; h[2 * q + 1] = w.y; }
 #pragma unroll
-        for (int q = 0; q < 18; ++q) { const double2 v = I2[q]; hi[2 * q] = v.x; hi[2 * q + 1] = v.y; }
+        for (int q = 0; q < 18; ++q) { const double2 w = I2[q]; li[2 * q] = w.x; li[2 * q + 1] = w.y; }
         const bool gl = sgb[le] >= 0;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            double v = 0.0;
-            if (gl) {
+        for (int j = 0; j < 6; ++j) {   // U[i][j] = sum_{k <= j} Hgp[i][k] Li[j][k]
+            double w = 0.0;
 #pragma unroll
-                for (int k = 0; k < 6; ++k) v += hr[k] * hi[k * 6 + j];
-            }
-            y[j] = v;
+            for (int k = 0; k <= j; ++k) w += h[k] * li[6 * j + k];
+            u[j] = gl ? w : 0.0;
         }
-        double2* Y2 = reinterpret_cast<double2*>(sY + 36 * le + 6 * i);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {   // Y'[i][j] = sum_{k >= j} U[i][k] Li[k][j]
+            double w = 0.0;
+#pragma unroll
+            for (int k = j; k < 6; ++k) w += u[k] * li[6 * k + j];
+            y[j] = w;
+        }
         double2* G2 = reinterpret_cast<double2*>(a.Y + 36 * (size_t)(e0 + le) + 6 * i);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            Y2[q] = make_double2(y[2 * q], y[2 * q + 1]);
+            H2[q] = make_double2(u[2 * q], u[2 * q + 1]);
             G2[q] = make_double2(y[2 * q], y[2 * q + 1]);
         }
     }
     wave_sync_lds();
     SSTAMP(stp, 4, 0);
     // the photo's Schur pair products at their block-major slots: S_ab entries
-    // ([self] Hgg_a - Y'_a Hgp_b^T), r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
+    // ([self] Hgg_a - U_a U_b^T), r_a = [self] (gg_a - U_a v) and JTE_a = [self] gg_a
     for (int t = lane; t < 6 * npp; t += 64) {
         const int k = t / 6, i = t % 6;
         const int4 pp = ppl[k];   // {local e1, local e2, self | diagonal block << 1, slot offset}
-        const double2* Y2 = reinterpret_cast<const double2*>(sY + 36 * pp.x + 6 * i);
-        const double2* B2 = reinterpret_cast<const double2*>(sE + 90 * pp.y + 42);
+        const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * pp.x + 22 + 6 * i);
+        const double2* B2 = reinterpret_cast<const double2*>(sE + ES * pp.y + 22);
         double y[6], Hb[36];
 #pragma unroll
         for (int q = 0; q < 3; ++q) { const double2 v = Y2[q]; y[2 * q] = v.x; y[2 * q + 1] = v.y; }
@@ -2145,7 +2183,7 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
         for (int q = 0; q < 18; ++q) { const double2 v = B2[q]; Hb[2 * q] = v.x; Hb[2 * q + 1] = v.y; }
         double* out = a.pairprod + (size_t)pp.w;
         const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
-        const double* Hgg = sE + 90 * pp.x + 21;
+        const double* Hgg = sE + ES * pp.x;
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             double d = 0.0;
@@ -2156,17 +2194,13 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
                 const int r = i < j ? i : j, c = i < j ? j : i;
                 h = Hgg[r * 6 - r * (r - 1) / 2 + (c - r)];
             }
-#ifndef MCC_EXP_NO_PAIRSTORE
             out[i * 6 + j] = self ? h - d : -d;
-#else
-            if (d == 12345.0) out[i * 6 + j] = self ? h - d : -d;
-#endif
         }
         if (diag) {
             double d = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < 6; ++kk) d += y[kk] * sgs[kk];
-            const double gg = sE[90 * pp.x + 84 + i];
+            for (int kk = 0; kk < 6; ++kk) d += y[kk] * sv[kk];
+            const double gg = sE[ES * pp.x + 58 + i];
             out[36 + i] = self ? gg - d : 0.0;
             out[42 + i] = self ? gg : 0.0;
         }

@@ -5,7 +5,7 @@ diagnostic build (libmcc_diag.so).  Never quote this build's run time: read its 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_split.py [config] [views]
 
 Rows of the stamp buffer (32 slots each): k_photo photo p -> row p slots 0..5 (start, staged,
-sums, inverse, Y', pairs stored); k_prep workgroup w -> row w slots 8..11 (start, update,
+Cholesky, U / Y', pairs stored; slot 2 unused); k_prep workgroup w -> row w slots 8..11 (start, update,
 photo Rodrigues, edges stored); k_edge workgroup w -> row w / 2 slots 16 + 8 (w & 1) + 0..4
 (start, corners staged, sweep, butterfly, H stored).
 """
@@ -48,7 +48,7 @@ def main():
             print(f"  {n:22s} {med(d[:, k])}")
         print(f"  {'total':22s} {med(blk[ok][:, -1] - blk[ok][:, 0])}")
 
-    phases([0, 1, 2, 3, 4, 5], ["load+stage", "Hpp/gp sums", "6x6 inverse", "Y'", "pairs+store"], "k_photo")
+    phases([0, 1, 3, 4, 5], ["load+stage+sums", "Cholesky, Li", "U, Y'", "pairs+store"], "k_photo")
     phases([8, 9, 10, 11], ["photo update", "photo Rodrigues", "edge prologues"], "k_prep")
     for h in (0, 1):
         base = 16 + 8 * h

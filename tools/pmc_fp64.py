@@ -40,8 +40,15 @@ def main():
         e["launches"] = max(e["launches"], len(v))
     for e in kernels.values():
         e["fp64_flops"] = 64.0 * (e.get("SQ_INSTS_VALU_FLOPS_FP64", 0.0) + e.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0))
-    lin = kernels.get("k_linearize", {})
-    out = {"config": a.config, "n_views": a.views, "kernel": "k_linearize",
+    for e in kernels.values():
+        e["fp64_flops_per_corner"] = e["fp64_flops"] / a.corners if a.corners else None
+    step_kernels = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
+    step = sum(kernels[k]["fp64_flops"] for k in step_kernels)
+    lin_k = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo") if k in kernels]
+    lin = {"fp64_flops": sum(kernels[k]["fp64_flops"] for k in lin_k)} if lin_k else {}
+    out = {"config": a.config, "n_views": a.views, "kernel": "+".join(lin_k),
+           "step_kernels": step_kernels, "step_fp64_flops": step,
+           "step_fp64_flops_per_corner": step / a.corners if a.corners else None,
            "fp64_flops_per_launch": lin.get("fp64_flops"),
            "fp64_flops_per_corner": (lin.get("fp64_flops", 0.0) / a.corners) if a.corners else None,
            "method": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass); flops = 64 x (FLOPS_FP64 + "
@@ -50,7 +57,7 @@ def main():
            "kernels": kernels}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps({k: out[k] for k in ("fp64_flops_per_launch", "fp64_flops_per_corner")}))
+    print(json.dumps({k: out[k] for k in ("fp64_flops_per_launch", "fp64_flops_per_corner", "step_fp64_flops_per_corner")}))
 
 
 if __name__ == "__main__":

@@ -37,7 +37,7 @@ def read_counters(d):
 
 
 def short(name):
-    for k in ("k_linearize", "k_schur", "k_solve", "k_backsub", "k_project_error"):
+    for k in ("k_linearize", "k_schur", "k_solve", "k_backsub", "k_project_error", "k_prep", "k_edge", "k_photo"):
         if k in name:
             return k
     return name
@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--config", default="config2")
     ap.add_argument("--views", type=int, default=500)
     ap.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per k_linearize launch")
+    ap.add_argument("--fetch-correction", type=float, default=2.0,
+                    help="FETCH_SIZE multiplier (2 = the guide's 16-B-per-lane figure; tools/fetch_calib.hip measures others)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     fv, wv = read_counters(a.fetch), read_counters(a.write)
@@ -64,19 +66,24 @@ def main():
         elif cn.startswith("WRITE_SIZE"):
             e["write_kib"] = mean
     for k, e in kernels.items():
-        fb = 2.0 * 1024.0 * e.get("fetch_kib_raw", 0.0)
+        fb = a.fetch_correction * 1024.0 * e.get("fetch_kib_raw", 0.0)
         wb = 1024.0 * e.get("write_kib", 0.0)
         e["read_bytes_corrected"] = fb
         e["write_bytes"] = wb
         e["bytes_per_launch"] = fb + wb
-    lin = kernels.get("k_linearize", {})
+    step_kernels = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
+    step_bytes = sum(kernels[k]["bytes_per_launch"] for k in step_kernels)
+    lin_k = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo") if k in kernels]
+    lin = {"bytes_per_launch": sum(kernels[k]["bytes_per_launch"] for k in lin_k)} if lin_k else {}
     out = {
-        "config": a.config, "n_views": a.views, "kernel": "k_linearize",
+        "config": a.config, "n_views": a.views, "kernel": "+".join(lin_k),
+        "step_kernels": step_kernels, "step_bytes_per_launch": step_bytes,
+        "step_ratio_to_alg": (step_bytes / a.alg_bytes) if a.alg_bytes else None,
         "bytes_per_launch": lin.get("bytes_per_launch"),
         "alg_bytes_per_launch": a.alg_bytes,
         "ratio_to_alg": (lin["bytes_per_launch"] / a.alg_bytes) if (a.alg_bytes and lin) else None,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
-                  "bytes = 2 x 1024 x FETCH_SIZE(KiB) [gfx950 correction] + 1024 x WRITE_SIZE(KiB); "
+                  f"bytes = {a.fetch_correction:g} x 1024 x FETCH_SIZE(KiB) [gfx950 correction] + 1024 x WRITE_SIZE(KiB); "
                   "memory-side (L2 -> fabric) bytes incl. Infinity-Cache hits",
         "kernels": kernels,
     }
