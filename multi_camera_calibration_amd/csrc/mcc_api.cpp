@@ -137,14 +137,15 @@ struct mcc_problem {
     long long corners = 0;
     bool rational = false, prism = false;
     int has_back = 0;
-    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0, max_ppp = 0;
+    int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
     size_t n_pair_doubles = 0;   // Schur pair-product slots (36 or 48 doubles each)
+    // split step's k_photo groups (consecutive photos) and their pair / contribution lists
+    int n_pgroups = 0, max_gpairs = 0, max_gcon = 0, max_gedges = 0;
+    size_t photo_shmem = 0;
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
-    // m > 30 (or MCC_FUSED=0): the split step k_prep -> k_edge -> k_photo (MCC_SPLIT=0: the
-    // earlier single per-photo k_linearize)
-    int split = 1;
+    // m > 30 (or MCC_FUSED=0): the split step k_prep -> k_edge -> k_photo -> k_schur -> k_solve
     int max_cpp = 1;   // most corners of one photo
     hipStream_t stream = nullptr;
 
@@ -158,8 +159,10 @@ struct mcc_problem {
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
-    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk, photo_pair_ptr;
-    DevBuf<int4> edge_info, items, photo_pairs;
+    DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
+    DevBuf<int> pgrp_ptr, gpair_ptr, gcon_ptr;
+    DevBuf<unsigned> gcon;
+    DevBuf<int4> edge_info, items, gpairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
     int packed_len = 0, ntri = 0;
@@ -233,8 +236,9 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
     la.Y = p->Y.p; la.zp = p->zp.p;
-    la.photo_pair_ptr = p->photo_pair_ptr.p; la.photo_pairs = p->photo_pairs.p; la.pairprod = p->pairprod.p;
-    la.max_ppp = p->fused ? 0 : p->max_ppp;
+    la.pgrp_ptr = p->pgrp_ptr.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
+    la.gcon_ptr = p->gcon_ptr.p; la.gcon = p->gcon.p; la.pairprod = p->pairprod.p;
+    la.n_pgroups = p->n_pgroups; la.max_gpairs = p->max_gpairs; la.max_gcon = p->max_gcon; la.max_gedges = p->max_gedges;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
     la.gblock = p->edge_gblock.p;
@@ -256,8 +260,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.n_edges = p->E; la.n_photos = p->V;
     la.erec = p->erec.p; la.echain = p->echain.p; la.eh = p->eh.p;
     if (p->V > 0) {
-        if (!p->fused && p->split)
-            HIPCHK(mcc_launch_split(la, p->model, p->max_epp, p->max_ppp, p->rational, p->prism, p->stream));
+        if (!p->fused)
+            HIPCHK(mcc_launch_split(la, p->model, p->rational, p->prism, p->photo_shmem, p->stream));
         else
             HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     }
@@ -513,28 +517,62 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         p->max_cpp = std::max(p->max_cpp, photo_corner[v + 1] - photo_corner[v]);
     }
 
-    // ---- Schur pair lists grouped by camera-pair block, chunked into work items
+    // ---- Schur pair lists.  k_photo (split step) takes groups of consecutive photos (at most
+    // kPhotoGroup photos / kPhotoGroupEdges edges) and sums the group's pair products per
+    // camera-pair block: one slot per (group, block), block-major over the groups, k_schur sums a
+    // block's slots in order.  A contribution is one ordered edge pair (e1, e2) of a photo with
+    // gblock(e1) <= gblock(e2) (both orders within one block), in photo then edge order.
     const int nb = p->m / 6;
     p->nblk = nb * (nb + 1) / 2;
     auto blk_index = [nb](int b1, int b2) { return b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1); };
-    // photo-major: {local e1, local e2, self, block-major slot}; k_linearize writes each pair's
-    // product at its slot, k_schur sums a block's slots in order
-    std::vector<int4> photo_pairs;
-    std::vector<int> photo_pair_ptr(V + 1, 0);
-    std::vector<std::vector<int>> blk_src(p->nblk);   // photo-major index of each block's pairs
-    for (int v = 0; v < V; ++v) {
-        for (int e1 = photo_ptr[v]; e1 < photo_ptr[v + 1]; ++e1) {
-            if (gblock[e1] < 0) continue;
-            for (int e2 = photo_ptr[v]; e2 < photo_ptr[v + 1]; ++e2) {
-                if (gblock[e2] < 0 || gblock[e1] > gblock[e2]) continue;
-                blk_src[blk_index(gblock[e1], gblock[e2])].push_back((int)photo_pairs.size());
-                photo_pairs.push_back(make_int4(e1 - photo_ptr[v], e2 - photo_ptr[v],
-                                                (e1 == e2 ? 1 : 0) | (gblock[e1] == gblock[e2] ? 2 : 0), -1));
-            }
+    std::vector<int> pgrp_ptr(1, 0);
+    for (int v = 0; v < V;) {
+        int w = v, edges = 0;
+        while (w < V && w - v < mcc::kPhotoGroup &&
+               (w == v || edges + (photo_ptr[w + 1] - photo_ptr[w]) <= mcc::kPhotoGroupEdges)) {
+            edges += photo_ptr[w + 1] - photo_ptr[w];
+            ++w;
         }
-        photo_pair_ptr[v + 1] = (int)photo_pairs.size();
-        p->max_ppp = std::max(p->max_ppp, photo_pair_ptr[v + 1] - photo_pair_ptr[v]);
+        pgrp_ptr.push_back(w);
+        v = w;
     }
+    const int NG = (int)pgrp_ptr.size() - 1;
+    std::vector<int4> gpairs;                           // {first contribution, count, diagonal << 1, slot}
+    std::vector<unsigned> gcon;
+    std::vector<int> gpair_ptr(NG + 1, 0), gcon_ptr(NG + 1, 0);
+    std::vector<std::vector<int>> blk_src(p->nblk);   // each block's gpairs, group order
+    std::vector<std::vector<unsigned>> per_blk(p->nblk);
+    for (int g = 0; g < NG; ++g) {
+        const int ge0 = photo_ptr[pgrp_ptr[g]];
+        std::vector<int> used;
+        for (int v = pgrp_ptr[g]; v < pgrp_ptr[g + 1]; ++v)
+            for (int e1 = photo_ptr[v]; e1 < photo_ptr[v + 1]; ++e1) {
+                if (gblock[e1] < 0) continue;
+                for (int e2 = photo_ptr[v]; e2 < photo_ptr[v + 1]; ++e2) {
+                    if (gblock[e2] < 0 || gblock[e1] > gblock[e2]) continue;
+                    const int b = blk_index(gblock[e1], gblock[e2]);
+                    if (per_blk[b].empty()) used.push_back(b);
+                    per_blk[b].push_back((unsigned)(e1 - ge0) | ((unsigned)(e2 - ge0) << 8) |
+                                         ((e1 == e2 ? 1u : 0u) << 16) | ((unsigned)(v - pgrp_ptr[g]) << 17));
+                }
+            }
+        std::sort(used.begin(), used.end());
+        const int cbase = (int)gcon.size();
+        for (int b : used) {
+            blk_src[b].push_back((int)gpairs.size());
+            const int b1 = [&] { int r = 0; while (r + 1 < nb && blk_index(r + 1, r + 1) <= b) ++r; return r; }();
+            gpairs.push_back(make_int4((int)gcon.size() - cbase, (int)per_blk[b].size(), blk_index(b1, b1) == b ? 2 : 0, -1));
+            gcon.insert(gcon.end(), per_blk[b].begin(), per_blk[b].end());
+            per_blk[b].clear();
+        }
+        gpair_ptr[g + 1] = (int)gpairs.size();
+        gcon_ptr[g + 1] = (int)gcon.size();
+        p->max_gpairs = std::max(p->max_gpairs, gpair_ptr[g + 1] - gpair_ptr[g]);
+        p->max_gcon = std::max(p->max_gcon, gcon_ptr[g + 1] - gcon_ptr[g]);
+        p->max_gedges = std::max(p->max_gedges, photo_ptr[pgrp_ptr[g + 1]] - ge0);
+    }
+    p->n_pgroups = NG;
+    p->photo_shmem = mcc::photo_lds_bytes(p->max_gedges, p->max_gpairs, p->max_gcon);
     std::vector<int4> items;
     std::vector<int> block_items(p->nblk + 1, 0);
     // slot sizes: 48 doubles on a diagonal camera-pair block (S entries, r, JTE), 36 off the
@@ -542,6 +580,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // doubles; item = {block, first slot's offset, slots, slot size}
     int n_slots = 0;
     size_t n_doubles = 0;
+    int min_slots = 160;
+    if (const char* f = std::getenv("MCC_ITEM_SLOTS")) min_slots = std::max(1, std::atoi(f));
     for (int b = 0; b < p->nblk; ++b) {
         int b1 = 0;
         while (b1 + 1 < nb && blk_index(b1 + 1, b1 + 1) <= b) ++b1;
@@ -549,15 +589,16 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         const int begin = n_slots;
         const size_t base = n_doubles;
         for (int src : blk_src[b]) {
-            photo_pairs[src].w = (int)n_doubles;
+            gpairs[src].w = (int)n_doubles;
             n_doubles += stride;
             ++n_slots;
         }
         if (n_doubles > (size_t)INT32_MAX) return bail(fail(MCC_EINVAL, "too many Schur pairs"));
         const int end = n_slots;
-        // <= 24 work items per block keeps the last-arriver assembly short; >= 20 pairs per item
-        // (4 per sub-chunk thread) keeps the item workgroups busy
-        const int per_item = std::max(20, (end - begin + 23) / 24);
+        // <= 24 work items per block keeps the last-arriver assembly short; >= min_slots slots per
+        // item (MCC_ITEM_SLOTS, default 160) amortises an item's fixed latency (one load round trip, the
+        // write-through hand-off and ticket) over more slots
+        const int per_item = std::max(min_slots, (end - begin + 23) / 24);
         for (int s = begin; s < end; s += per_item)
             items.push_back(make_int4(b, (int)(base + (size_t)(s - begin) * stride), std::min(end, s + per_item) - s, stride));
         // a block no photo couples gets one empty item: its last arriver writes the block's zeros
@@ -577,8 +618,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // small camera blocks: one kernel per Gauss-Newton step (MCC_FUSED=0 forces the k_schur path)
     p->fused = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
     if (const char* f = std::getenv("MCC_FUSED")) p->fused = p->fused && std::atoi(f) != 0;
-    if (const char* f = std::getenv("MCC_SPLIT")) p->split = std::atoi(f) != 0;
-    if (!p->fused && p->split && p->max_epp > 64)
+    if (!p->fused && p->max_epp > 64)
         return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;
@@ -625,14 +665,17 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->cam_pose.upload(cp.data(), 16 * C));
     HIPC(p->ds_rt.upload(ds_rt, 6));
     HIPC(p->alpha.upload(alpha.data(), alpha.size()));
-    HIPC(p->photo_pairs.upload(photo_pairs.data(), photo_pairs.size()));
-    HIPC(p->photo_pair_ptr.upload(photo_pair_ptr.data(), V + 1));
+    HIPC(p->pgrp_ptr.upload(pgrp_ptr.data(), pgrp_ptr.size()));
+    HIPC(p->gpair_ptr.upload(gpair_ptr.data(), gpair_ptr.size()));
+    HIPC(p->gpairs.upload(gpairs.data(), gpairs.size()));
+    HIPC(p->gcon_ptr.upload(gcon_ptr.data(), gcon_ptr.size()));
+    HIPC(p->gcon.upload(gcon.data(), gcon.size()));
     HIPC(p->items.upload(items.data(), items.size()));
     HIPC(p->block_items.upload(block_items.data(), block_items.size()));
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E));
     HIPC(p->pairprod.alloc(p->fused ? 0 : p->n_pair_doubles));
-    const bool use_split = !p->fused && p->split;
+    const bool use_split = !p->fused;
     HIPC(p->erec.alloc(use_split ? 12 * (size_t)E : 0));
     HIPC(p->echain.alloc(use_split ? 54 * (size_t)E : 0));
     HIPC(p->eh.alloc(use_split ? 90 * (size_t)E : 0));
@@ -665,9 +708,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->h_state->change = 1.0;
     HIPC(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
-    if (mcc_lin_shmem(p->max_epp, C, p->m, p->fused, p->max_cpp, p->max_ppp) > 160 * 1024)
+    if (p->fused && mcc_lin_shmem(p->max_epp, C, p->m, p->max_cpp) > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many edges / corners per photo for the LDS staging"));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->fused, p->max_cpp, p->max_ppp));
+    if (!p->fused && p->photo_shmem > 160 * 1024)
+        return bail(fail(MCC_EINVAL, "too many Schur pairs of one photo for k_photo's LDS"));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -697,8 +742,8 @@ void mcc_destroy(mcc_problem* p) {
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
-    p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->photo_pairs.release();
-    p->photo_pair_ptr.release();
+    p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->gpairs.release();
+    p->pgrp_ptr.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused

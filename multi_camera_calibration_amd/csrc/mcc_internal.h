@@ -63,11 +63,16 @@ struct LinArgs {
     int nd, global_dim, n_cams, has_back;
     // outputs
     double* Y;        // [36E] Schur factors Y'_e = Hgp_e Hpp^-1
-    // k_schur path: the photo's Schur pair products, [48] per pair at its block-major slot
-    const int* photo_pair_ptr;   // [V+1] photo-major ranges of photo_pairs
-    const int4* photo_pairs;     // {local e1, local e2, self | diagonal block << 1, slot offset (doubles)}
-    double* pairprod;            // per pair {S_ab entries (36), [diagonal block] r_a (6), JTE_a (6)}
-    int max_ppp;                 // most pairs of one photo (LDS staging)
+    // split step: k_photo runs over groups of consecutive photos (<= kPhotoGroup photos and
+    // <= kPhotoGroupEdges edges); each group sums its photos' Schur pair products per camera-pair
+    // block and writes them at that block's slot (block-major over the groups; k_schur sums them)
+    const int* pgrp_ptr;     // [n_pgroups + 1] first photo of each group
+    const int* gpair_ptr;    // [n_pgroups + 1] ranges of gpairs
+    const int4* gpairs;      // {first contribution (group-relative), count, diagonal block << 1, slot offset}
+    const int* gcon_ptr;     // [n_pgroups + 1] ranges of gcon
+    const unsigned* gcon;    // contribution: edge a | edge b << 8 | self << 16 | photo << 17 (group-local)
+    double* pairprod;        // per slot {S_ab entries (36), [diagonal block] r_a (6), JTE_a (6)}
+    int n_pgroups, max_gpairs, max_gcon, max_gedges;
     double* zp;       // [6V] z' = Hpp^-1 gp
     double* gp_tot;   // [6V] photo JTE
     float* resid;     // optional [2*corners] float32 residuals (debug)
@@ -95,10 +100,16 @@ struct LinArgs {
     double* eh;              // [90E] Hpp upper (21), Hgg upper (21), Hgp (36), gp (6), gg (6) (k_edge -> k_photo)
 };
 
-// k_photo's LDS: per edge [Hgg upper 21 | pad | U 36 | gg 6] (64 doubles), the Hpp / gp sums [28],
-// Hpp's inverse Cholesky factor [36], v [6], gblock [ne] ints, then (16-B aligned) the Schur pairs
-__host__ __device__ inline size_t photo_lds_doubles(int ne) {
-    return ((size_t)64 * ne + 70 + (size_t)(ne + 1) / 2 + 1) & ~(size_t)1;
+constexpr int kPhotoGroup = 8;        // photos per k_photo workgroup, at most
+constexpr int kPhotoGroupEdges = 64;  // edges per k_photo workgroup, at most
+// k_photo's LDS (doubles, then ints): per edge [Hgg upper 21 | pad | U 36 | gg 6] (64), per photo the
+// Hpp / gp sums [28], Hpp's inverse Cholesky factor Li [36] and v [6]; then per edge gblock and
+// photo (ints), the group's pairs (int4) and contributions (unsigned)
+__host__ __device__ inline size_t photo_lds_doubles(int gne) {
+    return (size_t)64 * gne + (size_t)70 * kPhotoGroup;
+}
+__host__ __device__ inline size_t photo_lds_bytes(int gne, int npairs, int ncon) {
+    return photo_lds_doubles(gne) * 8 + 4 * (size_t)((2 * gne + 3) & ~3) + 16 * (size_t)npairs + 4 * (size_t)ncon;
 }
 
 struct SchurArgs {
@@ -151,11 +162,10 @@ struct ErrArgs {
 }  // namespace mcc
 
 // launch wrappers (mcc_kernels.hip)
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp);
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp, int max_ppp);
-size_t mcc_photo_shmem(int max_epp, int max_ppp);
-hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, int max_epp, int max_ppp, bool rational, bool prism,
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem);
+hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
                             hipStream_t s);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);

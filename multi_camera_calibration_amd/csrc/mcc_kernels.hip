@@ -867,9 +867,8 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
-// FUSED: the m <= 30 single-kernel step (a.fused); !FUSED: the k_schur path's linearisation.  Two
-// instantiations, so neither carries the other's code.
-template <int MODEL, bool RATIONAL, bool PRISM, bool FUSED>
+// The m <= 30 single-kernel step (a.fused); m > 30 takes the split step below.
+template <int MODEL, bool RATIONAL, bool PRISM>
 __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
     const int photo = blockIdx.x;
@@ -879,8 +878,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     const double alpha_prev = st->alpha;   // step factor of the pending update
     const int e0 = a.photo_ptr[photo];
     const int ne = a.photo_ptr[photo + 1] - e0;
-    const int pp0 = FUSED ? 0 : a.photo_pair_ptr[photo];
-    const int npp = FUSED ? 0 : a.photo_pair_ptr[photo + 1] - pp0;
     if (done) return;
     STAMP(0);
     RSTAMP(14);
@@ -898,7 +895,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][kCamStride] = {R, Jl, T}
     double* ktab = ctab + kCamStride * a.n_cams;         // [C][kIntrStride] intrinsics
     float* cs = reinterpret_cast<float*>(ktab + kIntrStride * a.n_cams);   // [5][max_cpp] corners
-    int4* ppl = reinterpret_cast<int4*>(reinterpret_cast<char*>(cs) + ((5 * sizeof(float) * a.max_cpp + 15) & ~(size_t)15));
     const int c0 = a.photo_corner[photo];
     const int ncs = a.photo_corner[photo + 1] - c0;
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
@@ -913,7 +909,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
         else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
         else if (lane == 10) P.iter0 = st->iter;
-        if (FUSED && pending) {
+        if (pending) {
             if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
             // W (written by the previous step) is indexed by the photo alone, so every operand
@@ -930,38 +926,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 }
 #pragma unroll
                 for (int u = 0; u < 3; ++u) part += w[u] * d[u];
-            }
-        } else if (pending) {
-            if (lane >= 42 && lane < 48) lov = a.zp[6 * (size_t)photo + lane - 42];   // z' = Hpp^-1 gp
-            // lane l < 60: k = l % 6, edges l / 6, l / 6 + 10, ...: sum_i Y_e[i][k] dg_{g(e)}[i].
-            // The first edge's Y column and block are loaded before dg is staged, so the two
-            // global round trips overlap.
-            const int k = lane % 6, le0 = lane / 6;
-            const bool has0 = lane < 60 && le0 < ne;
-            double y0[6];
-            int g0 = -1;
-            if (has0) {
-                g0 = a.gblock[e0 + le0];
-                const double* Ye = a.Y + 36 * (size_t)(e0 + le0) + k;
-#pragma unroll
-                for (int i = 0; i < 6; ++i) y0[i] = Ye[6 * i];
-            }
-            for (int q = lane; q < a.global_dim; q += 64) P.dgl[q] = a.dg[q];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (has0 && g0 >= 0) {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) part += y0[i] * P.dgl[6 * g0 + i];
-            }
-            if (lane < 60) {
-                for (int le = le0 + 10; le < ne; le += 10) {
-                    const int g = a.gblock[e0 + le];
-                    if (g < 0) continue;
-                    const double* Ye = a.Y + 36 * (size_t)(e0 + le) + k;
-#pragma unroll
-                    for (int i = 0; i < 6; ++i) part += Ye[6 * i] * P.dgl[6 * g + i];
-                }
             }
         }
     } else if (wave == 1) {
@@ -1017,9 +981,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             EdgeLds& L = el[le];
             L.cam = info.x; L.side = info.y; L.off = info.z - c0; L.n = info.w; L.edge = e0 + le;
         }
-        // k_schur path: the photo's Schur pairs (local edges, self, block-major slot)
-        if (!FUSED)
-            for (int q = tid - 128; q < npp; q += 128) ppl[q] = a.photo_pairs[pp0 + q];
         // the photo's corners are contiguous (photo-major layout): stage all five streams
         for (int q = tid - 128; q < ncs; q += 128) {
             const size_t c = (size_t)c0 + q;
@@ -1032,7 +993,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     }
     STAMP(16);
     if (wave == 0) {
-        if (FUSED && pending) {
+        if (pending) {
             // fused back-substitution of the previous step: dp_k = z'_k - sum_c part(k, c),
             // the ten partials of component k summed in c order through LDS by lane k
             if (lane < 60) P.dgl[lane] = part;
@@ -1049,39 +1010,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
                 P.xp[lane] = xn;
                 P.dgl[64 + lane] = (double)G;
             }
-        } else if (pending) {
-            // fused back-substitution of the previous step: dp = z' - sum_e Y_e^T dg_e,
-            // operands gathered from wave 0's registers with compile-time v_readlane
-            double t[6];
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                double sacc = readlane_f64(lov, 42 + q);
-#pragma unroll
-                for (int j = 0; j < 10; ++j) sacc -= readlane_f64(part, 6 * j + q);
-                t[q] = sacc;
-            }
-            double g2 = 0.0, x2 = 0.0;
-#pragma unroll
-            for (int q = 0; q < 6; ++q) {
-                const float G = (float)(alpha_prev * t[q]);   // G = alpha*delta -> CV_32F (:491-496)
-                const float xn = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xov), q)) + G;   // x = x + G (:501)
-                if (lane == q) { xg[q] = xn; P.xp[q] = xn; }
-                g2 += (double)G * (double)G;
-                x2 += (double)xn * (double)xn;
-            }
-            if (lane == 0) {
-                a.photo_norm[2 * (size_t)photo] = g2;
-                a.photo_norm[2 * (size_t)photo + 1] = x2;
-                P.nrm[0] = g2;
-                P.nrm[1] = x2;
-            }
         } else if (lane < 6) {
             P.xp[lane] = xov;
         }
         STAMP(18);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         if (lane == 0) {   // photo Rodrigues, shared by every edge of the photo
-            if (FUSED && pending) {   // norms of the applied update (independent of the Rodrigues chain)
+            if (pending) {   // norms of the applied update (independent of the Rodrigues chain)
                 double g2 = 0.0, x2 = 0.0;
 #pragma unroll
                 for (int q = 0; q < 6; ++q) {
@@ -1281,54 +1216,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     for (int t = tid; t < 36 * ne; t += blockDim.x) {
         const int le = t / 36, ij = t % 36, i = ij / 6, j = ij % 6;
         EdgeLds& L = el[le];
-        const size_t e = (size_t)(e0 + le);
         double y = 0.0;
         if (L.has_global) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) y += L.Hgp[i * 6 + k] * Hi[k * 6 + j];
         }
-        L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the products below
-        if (!FUSED) a.Y[36 * e + ij] = y;   // (fused: W below replaces the edge-indexed Y')
+        L.Xg[ij] = y;   // Xg (A' Gg scratch) is dead: Y'_e for the products below (W replaces the edge-indexed Y')
     }
-    if (!FUSED) {
-        // k_schur path: the photo's Schur pair products, each at its block-major slot, so k_schur
-        // streams and sums them in slot order:  S_ab entries ([self] Hgg_a - Y'_a Hgp_b^T),
-        // r_a = [self] (gg_a - Y'_a gp) and JTE_a = [self] gg_a
-        // thread (pair k, row i): row i of the 6x6 product and entry i of r and JTE
-        __syncthreads();
-        for (int t = tid; t < 6 * npp; t += blockDim.x) {
-            const int k = t / 6, i = t % 6;
-            const int4 pp = ppl[k];   // {local e1, local e2, self, slot}
-            const EdgeLds& La = el[pp.x];
-            const EdgeLds& Lb = el[pp.y];
-            double y[6];
-#pragma unroll
-            for (int kk = 0; kk < 6; ++kk) y[kk] = La.Xg[i * 6 + kk];
-            double* out = a.pairprod + (size_t)pp.w;   // 48-double slot on a diagonal block, else 36
-            const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double d = 0.0;
-#pragma unroll
-                for (int kk = 0; kk < 6; ++kk) d += y[kk] * Lb.Hgp[j * 6 + kk];
-                out[i * 6 + j] = self ? La.Hgg[i * 6 + j] - d : -d;
-            }
-            if (diag) {
-                double d = 0.0;
-#pragma unroll
-                for (int kk = 0; kk < 6; ++kk) d += y[kk] * gs[kk];
-                out[36 + i] = self ? La.gg[i] - d : 0.0;
-                out[42 + i] = self ? La.gg[i] : 0.0;
-            }
-        }
-#ifdef MCC_DIAG
-        __syncthreads();
-        STAMP(7);
-        RSTAMP(15);
-#endif
-        return;
-    }
-
     if (tid >= 192 && tid < 197) {   // per camera block (m <= 30: at most 5) the photo's edges in edge order
         const int b = tid - 192;
         int cnt = 0;
@@ -2008,78 +1902,102 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     SSTAMP(stp, 4, 0);
 }
 
-// One wave per photo vertex: Hpp = sum_e Hpp_e and gp (edge order), its Cholesky factor Hpp = L L^T
-// and Li = L^-1 (so Hpp^-1 = Li^T Li), z' = Hpp^-1 gp, per edge U_e = Hgp_e Li^T (in place of Hgp)
-// and Y'_e = Hgp_e Hpp^-1 = U_e Li (-> Y, the next step's photo update), and the photo's Schur pair
-// products Y'_a Hgp_b^T = U_a U_b^T at their block-major slots (k_schur).  Keeping U instead of both
-// Y' and Hgp halves the LDS per edge (64 doubles), so more photos' chains overlap per CU.
-__global__ __launch_bounds__(64) void k_photo(LinArgs a) {
+// One workgroup per group of consecutive photo vertices (at most kPhotoGroup photos and
+// kPhotoGroupEdges edges, host-built).  Per photo: Hpp = sum_e Hpp_e and gp (edge order), the
+// Cholesky factor Hpp = L L^T and Li = L^-1 (so Hpp^-1 = Li^T Li), z' = Hpp^-1 gp; per edge
+// U_e = Hgp_e Li^T (in place of Hgp) and Y'_e = Hgp_e Hpp^-1 = U_e Li (-> Y, the next step's photo
+// update).  Then per camera-pair block the group touches: the sum over its photos' edge pairs of
+// the Schur pair products ([self] Hgg_a - Y'_a Hgp_b^T = U_a U_b^T, [self] (gg_a - U_a v),
+// [self] gg_a), written once per group at the block's slot (k_schur sums the slots).  Summing in
+// the group first cuts the slots (and k_schur's reads) to ~40% at 8 photos per group on config3.
+__global__ __launch_bounds__(256) void k_photo(LinArgs a) {
     State* st = a.state;
     if (st->done) return;
-    const int photo = blockIdx.x, lane = threadIdx.x;
-    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)photo : nullptr;   // MCC_DIAG: slots 0..7
+    const int grp = blockIdx.x, tid = threadIdx.x;
+    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)grp : nullptr;   // MCC_DIAG: slots 0..7
     SSTAMP(stp, 0, 0);
-    const int e0 = a.photo_ptr[photo], ne = a.photo_ptr[photo + 1] - e0;
-    const int pp0 = a.photo_pair_ptr[photo], npp = a.photo_pair_ptr[photo + 1] - pp0;
+    const int p0 = a.pgrp_ptr[grp], np = a.pgrp_ptr[grp + 1] - p0;
+    const int ge0 = a.photo_ptr[p0], gne = a.photo_ptr[p0 + np] - ge0;   // the group's edges are contiguous
+    const int q0 = a.gpair_ptr[grp], nq = a.gpair_ptr[grp + 1] - q0;
+    const int c0 = a.gcon_ptr[grp], nc = a.gcon_ptr[grp + 1] - c0;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    constexpr int ES = 64;               // per edge: Hgg upper [0, 21), pad, U [22, 58), gg [58, 64)
-    double* sE = smem;                   // [ne][ES]
-    double* s27 = sE + ES * ne;          // [28]: Hpp upper 21, gp 6
-    double* sLi = s27 + 28;              // [36]: Li = L^-1 (lower, zeros above)
-    double* sv = sLi + 36;               // [6]:  v = Li gp
-    int* sgb = reinterpret_cast<int*>(sv + 6);                                    // [ne]
-    int4* ppl = reinterpret_cast<int4*>(smem + photo_lds_doubles(ne));            // [npp]
-    const double* src = a.eh + 90 * (size_t)e0;   // eh = [Hpp 21 | Hgg 21 | Hgp 36 | gp 6 | gg 6]
+    constexpr int ES = 64;                      // per edge: Hgg upper [0, 21), pad, U [22, 58), gg [58, 64)
+    double* sE = smem;                          // [gne][ES]
+    double* s27 = sE + ES * gne;                // [kPhotoGroup][28]: Hpp upper 21, gp 6
+    double* sLi = s27 + 28 * kPhotoGroup;       // [kPhotoGroup][36]: Li = L^-1 (lower, zeros above)
+    double* sv = sLi + 36 * kPhotoGroup;        // [kPhotoGroup][6]: v = Li gp
+    int* sgb = reinterpret_cast<int*>(smem + photo_lds_doubles(gne));   // [gne] gblock
+    int* seq = sgb + gne;                                               // [gne] group-local photo
+    int4* spq = reinterpret_cast<int4*>(sgb + ((2 * gne + 3) & ~3));   // [nq] (16-B aligned)
+    unsigned* scn = reinterpret_cast<unsigned*>(spq + nq);              // [nc]
+    const double* src = a.eh + 90 * (size_t)ge0;   // eh = [Hpp 21 | Hgg 21 | Hgp 36 | gp 6 | gg 6]
     {
-        // lanes < 27: the Hpp / gp column sums in edge order, loaded straight to registers (the
-        // first 16 edges' loads issued before the staging's); every lane: the rest of eh -> LDS
+        // every load of the staging issued before the first LDS store: the rest of eh -> LDS
+        // (16 per thread: one round up to 64 edges); threads < 27 np: photo q's Hpp / gp column
+        // sums in edge order, straight to registers
+        constexpr int U = 16;
+        const int tot = ES * gne;
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = tid + 256 * u, le = t >> 6, c = t & 63;
+            const int sc = c < 21 ? c + 21 : (c < 58 ? c + 20 : c + 26);
+            v[u] = src[t < tot ? 90 * le + sc : 0];
+        }
+        const int sq = tid / 27, col27 = tid % 27;
+        const bool sl = sq < np;
+        int pe0 = 0, pne = 0;
+        if (sl) {
+            pe0 = a.photo_ptr[p0 + sq] - ge0;
+            pne = a.photo_ptr[p0 + sq + 1] - ge0 - pe0;
+        }
+        const int col = col27 < 21 ? col27 : 78 + (col27 - 21);
         constexpr int SB = 16;
-        const bool sl = lane < 27;
-        const int col = lane < 21 ? lane : 78 + (lane - 21);
         double sv0[SB];
 #pragma unroll
-        for (int u = 0; u < SB; ++u) sv0[u] = (sl && u < ne) ? src[90 * u + col] : 0.0;
-        const int4 pq0 = lane < npp ? a.photo_pairs[pp0 + lane] : make_int4(0, 0, 0, 0);
-        const int4 pq1 = lane + 64 < npp ? a.photo_pairs[pp0 + lane + 64] : make_int4(0, 0, 0, 0);
-        const int gbv = lane < ne ? a.gblock[e0 + lane] : -1;
-        constexpr int U = 16;
-        const int tot = ES * ne;
-        for (int t0 = 0; t0 < tot; t0 += 64 * U) {
-            double v[U];
+        for (int u = 0; u < SB; ++u) sv0[u] = (sl && u < pne) ? src[90 * (pe0 + u) + col] : 0.0;
+        const int gbv = tid < gne ? a.gblock[ge0 + tid] : -1;
+        const int4 pqv = tid < nq ? a.gpairs[q0 + tid] : make_int4(0, 0, 0, 0);
+        const unsigned cnv = tid < nc ? a.gcon[c0 + tid] : 0u;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + lane + 64 * u, le = t >> 6, c = t & 63;
-                const int sc = c < 21 ? c + 21 : (c < 58 ? c + 20 : c + 26);
-                v[u] = src[t < tot ? 90 * le + sc : 0];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int t = t0 + lane + 64 * u;
-                if (t < tot) sE[t] = v[u];
-            }
+        for (int u = 0; u < U; ++u) {
+            const int t = tid + 256 * u;
+            if (t < tot) sE[t] = v[u];
+        }
+        for (int t0 = 256 * U; t0 < tot; t0 += 256) {   // beyond 64 edges (host bounds the groups)
+            const int t = t0 + tid, le = t >> 6, c = t & 63;
+            const int sc = c < 21 ? c + 21 : (c < 58 ? c + 20 : c + 26);
+            if (t < tot) sE[t] = src[90 * le + sc];
         }
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < SB; ++u) s += sv0[u];
-        if (sl)
-            for (int le = SB; le < ne; ++le) s += src[90 * le + col];
-        if (sl) s27[lane] = s;
-        if (lane < ne) sgb[lane] = gbv;
-        for (int t = lane + 64; t < ne; t += 64) sgb[t] = a.gblock[e0 + t];
-        if (lane < npp) ppl[lane] = pq0;
-        if (lane + 64 < npp) ppl[lane + 64] = pq1;
-        for (int q = lane + 128; q < npp; q += 64) ppl[q] = a.photo_pairs[pp0 + q];
+        if (sl) {
+            for (int le = SB; le < pne; ++le) s += src[90 * (pe0 + le) + col];
+            s27[28 * sq + col27] = s;
+        }
+        if (tid < gne) sgb[tid] = gbv;
+        for (int t = tid + 256; t < gne; t += 256) sgb[t] = a.gblock[ge0 + t];
+        for (int q = 0; q < np; ++q) {   // edge -> group-local photo
+            const int b = a.photo_ptr[p0 + q] - ge0, e = a.photo_ptr[p0 + q + 1] - ge0;
+            for (int t = b + tid; t < e; t += 256) seq[t] = q;
+        }
+        if (tid < nq) spq[tid] = pqv;
+        for (int t = tid + 256; t < nq; t += 256) spq[t] = a.gpairs[q0 + t];
+        if (tid < nc) scn[tid] = cnv;
+        for (int t = tid + 256; t < nc; t += 256) scn[t] = a.gcon[c0 + t];
     }
-    wave_sync_lds();
+    __syncthreads();
     SSTAMP(stp, 1, 0);
-    if (lane == 0) {   // Cholesky Hpp = L L^T, Li = L^-1, v = Li gp, z' = Li^T v (registers, one lane)
+    if (tid < np) {   // one lane per photo: Cholesky Hpp = L L^T, Li = L^-1, v = Li gp, z' = Li^T v
+        const int q = tid, photo = p0 + q;
         double A[21], gs[6], Lm[6][6], Li[6][6];
-        const double2* S2 = reinterpret_cast<const double2*>(s27);
+        const double2* S2 = reinterpret_cast<const double2*>(s27 + 28 * q);
 #pragma unroll
-        for (int q = 0; q < 14; ++q) {
-            const double2 w = S2[q];
-            if (2 * q < 21) A[2 * q] = w.x; else gs[2 * q - 21] = w.x;
-            if (2 * q + 1 < 21) A[2 * q + 1] = w.y; else if (2 * q + 1 < 27) gs[2 * q + 1 - 21] = w.y;
+        for (int k = 0; k < 14; ++k) {
+            const double2 w = S2[k];
+            if (2 * k < 21) A[2 * k] = w.x; else gs[2 * k - 21] = w.x;
+            if (2 * k + 1 < 21) A[2 * k + 1] = w.y; else if (2 * k + 1 < 27) gs[2 * k + 1 - 21] = w.y;
         }
         bool bad = false;
         double idg[6];
@@ -2112,35 +2030,35 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
                 Li[i][j] = t * idg[i];
             }
         }
-        double v[6];
+        double vv[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             double t = 0.0;
 #pragma unroll
             for (int k = 0; k <= i; ++k) t += Li[i][k] * gs[k];
-            v[i] = t;
+            vv[i] = t;
         }
 #pragma unroll
         for (int j = 0; j < 6; ++j) {
             double t = 0.0;
 #pragma unroll
-            for (int i = j; i < 6; ++i) t += Li[i][j] * v[i];
+            for (int i = j; i < 6; ++i) t += Li[i][j] * vv[i];
             a.zp[6 * (size_t)photo + j] = t;
             a.gp_tot[6 * (size_t)photo + j] = gs[j];
-            sv[j] = v[j];
+            sv[6 * q + j] = vv[j];
         }
-        double2* L2 = reinterpret_cast<double2*>(sLi);
+        double2* L2 = reinterpret_cast<double2*>(sLi + 36 * q);
 #pragma unroll
-        for (int q = 0; q < 18; ++q) L2[q] = make_double2(Li[(2 * q) / 6][(2 * q) % 6], Li[(2 * q + 1) / 6][(2 * q + 1) % 6]);
+        for (int k = 0; k < 18; ++k) L2[k] = make_double2(Li[(2 * k) / 6][(2 * k) % 6], Li[(2 * k + 1) / 6][(2 * k + 1) % 6]);
         if (bad) atomicOr(&st->error, 1);
     }
-    wave_sync_lds();
+    __syncthreads();
     SSTAMP(stp, 3, 0);
-    for (int t = lane; t < 6 * ne; t += 64) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
+    for (int t = tid; t < 6 * gne; t += 256) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
         const int le = t / 6, i = t % 6;
         double h[6], li[36], u[6], y[6];
         double2* H2 = reinterpret_cast<double2*>(sE + ES * le + 22 + 6 * i);
-        const double2* I2 = reinterpret_cast<const double2*>(sLi);
+        const double2* I2 = reinterpret_cast<const double2*>(sLi + 36 * seq[le]);
 #pragma unroll
         for (int q = 0; q < 3; ++q) { const double2 w = H2[q]; h[2 * q] = w.x; h[2 * q + 1] = w.y; }
 #pragma unroll
@@ -2160,49 +2078,60 @@ __global__ __launch_bounds__(64) void k_photo(LinArgs a) {
             for (int k = j; k < 6; ++k) w += u[k] * li[6 * k + j];
             y[j] = w;
         }
-        double2* G2 = reinterpret_cast<double2*>(a.Y + 36 * (size_t)(e0 + le) + 6 * i);
+        double2* G2 = reinterpret_cast<double2*>(a.Y + 36 * (size_t)(ge0 + le) + 6 * i);
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
             H2[q] = make_double2(u[2 * q], u[2 * q + 1]);
             G2[q] = make_double2(y[2 * q], y[2 * q + 1]);
         }
     }
-    wave_sync_lds();
+    __syncthreads();
     SSTAMP(stp, 4, 0);
-    // the photo's Schur pair products at their block-major slots: S_ab entries
-    // ([self] Hgg_a - U_a U_b^T), r_a = [self] (gg_a - U_a v) and JTE_a = [self] gg_a
-    for (int t = lane; t < 6 * npp; t += 64) {
+    // task (block pair k, row i): the group's contributions summed in order (photo, then edge pair)
+    for (int t = tid; t < 6 * nq; t += 256) {
         const int k = t / 6, i = t % 6;
-        const int4 pp = ppl[k];   // {local e1, local e2, self | diagonal block << 1, slot offset}
-        const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * pp.x + 22 + 6 * i);
-        const double2* B2 = reinterpret_cast<const double2*>(sE + ES * pp.y + 22);
-        double y[6], Hb[36];
+        const int4 pq = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}
+        const bool diag = (pq.z & 2) != 0;
+        double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, racc = 0.0, jacc = 0.0;
+        for (int c = pq.x; c < pq.x + pq.y; ++c) {
+            const unsigned w = scn[c];
+            const int ea = w & 255, eb = (w >> 8) & 255, q = w >> 17;
+            const bool self = (w >> 16) & 1;
+            const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * ea + 22 + 6 * i);
+            const double2* B2 = reinterpret_cast<const double2*>(sE + ES * eb + 22);
+            double y[6], Hb[36];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) { const double2 v = Y2[q]; y[2 * q] = v.x; y[2 * q + 1] = v.y; }
+            for (int qq = 0; qq < 3; ++qq) { const double2 v = Y2[qq]; y[2 * qq] = v.x; y[2 * qq + 1] = v.y; }
 #pragma unroll
-        for (int q = 0; q < 18; ++q) { const double2 v = B2[q]; Hb[2 * q] = v.x; Hb[2 * q + 1] = v.y; }
-        double* out = a.pairprod + (size_t)pp.w;
-        const bool self = (pp.z & 1) != 0, diag = (pp.z & 2) != 0;
-        const double* Hgg = sE + ES * pp.x;
+            for (int qq = 0; qq < 18; ++qq) { const double2 v = B2[qq]; Hb[2 * qq] = v.x; Hb[2 * qq + 1] = v.y; }
+            const double* Hgg = sE + ES * ea;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            double d = 0.0;
+            for (int j = 0; j < 6; ++j) {
+                double d = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < 6; ++kk) d += y[kk] * Hb[j * 6 + kk];
-            double h = 0.0;
-            if (self) {
-                const int r = i < j ? i : j, c = i < j ? j : i;
-                h = Hgg[r * 6 - r * (r - 1) / 2 + (c - r)];
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * Hb[j * 6 + kk];
+                double h = 0.0;
+                if (self) {
+                    const int r = i < j ? i : j, cc = i < j ? j : i;
+                    h = Hgg[r * 6 - r * (r - 1) / 2 + (cc - r)];
+                }
+                acc[j] += self ? h - d : -d;
             }
-            out[i * 6 + j] = self ? h - d : -d;
-        }
-        if (diag) {
-            double d = 0.0;
+            if (diag && self) {
+                double d = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < 6; ++kk) d += y[kk] * sv[kk];
-            const double gg = sE[ES * pp.x + 58 + i];
-            out[36 + i] = self ? gg - d : 0.0;
-            out[42 + i] = self ? gg : 0.0;
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * sv[6 * q + kk];
+                const double gg = sE[ES * ea + 58 + i];
+                racc += gg - d;
+                jacc += gg;
+            }
+        }
+        double* out = a.pairprod + (size_t)pq.w;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) out[i * 6 + j] = acc[j];
+        if (diag) {
+            out[36 + i] = racc;
+            out[42 + i] = jacc;
         }
     }
 #ifdef MCC_DIAG
@@ -2925,17 +2854,12 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 // ---------------------------------------------------------------- launch wrappers
 using namespace mcc;
 
-template <int MODEL, bool FUSED>
-static void launch_lin_variant(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
-    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
-    else hipLaunchKernelGGL((k_linearize<MODEL, false, false, FUSED>), dim3(n_photos), dim3(256), shmem, s, a);
-}
 template <int MODEL>
 static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
-    if (a.fused) launch_lin_variant<MODEL, true>(a, n_photos, shmem, s, rational, prism);
-    else launch_lin_variant<MODEL, false>(a, n_photos, shmem, s, rational, prism);   // (MCC_FUSED=0 too)
+    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), dim3(n_photos), dim3(256), shmem, s, a);
+    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), dim3(n_photos), dim3(256), shmem, s, a);
+    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), dim3(n_photos), dim3(256), shmem, s, a);
     return hipGetLastError();
 }
 
@@ -2947,10 +2871,7 @@ static void launch_edge(const LinArgs& a, hipStream_t s) {
     constexpr int per = 64 / kEdgeLanes;
     hipLaunchKernelGGL((k_edge<MODEL, RATIONAL, PRISM, kEdgeLanes>), dim3((a.n_edges + per - 1) / per), dim3(64), 0, s, a);
 }
-size_t mcc_photo_shmem(int max_epp, int max_ppp) {
-    return photo_lds_doubles(max_epp) * sizeof(double) + sizeof(int4) * (size_t)max_ppp;
-}
-hipError_t mcc_launch_split(const LinArgs& a, int model, int max_epp, int max_ppp, bool rational, bool prism,
+hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
                             hipStream_t s) {
     if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
     const dim3 gp((a.n_photos + 64 / kPrepGroup - 1) / (64 / kPrepGroup));
@@ -2971,16 +2892,15 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, int max_epp, int max_pp
         else if (prism) launch_edge<MCC_MODEL_PINHOLE, false, true>(a, s);
         else launch_edge<MCC_MODEL_PINHOLE, false, false>(a, s);
     }
-    hipLaunchKernelGGL(k_photo, dim3(a.n_photos), dim3(64), mcc_photo_shmem(max_epp, max_ppp), s, a);
+    hipLaunchKernelGGL(k_photo, dim3(a.n_pgroups), dim3(256), photo_shmem, s, a);
     return hipGetLastError();
 }
 
-size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int fused, int max_cpp, int max_ppp) {
+size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
                        (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
-                       ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15) +
-                       (fused ? 0 : sizeof(int4) * (size_t)max_ppp);
-    return fused ? std::max(lin, (size_t)(m * m + m) * sizeof(double)) : lin;
+                       ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15);
+    return std::max(lin, (size_t)(m * m + m) * sizeof(double));
 }
 
 size_t mcc_solve_shmem(int m) {
@@ -2990,7 +2910,7 @@ size_t mcc_solve_shmem(int m) {
 }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.fused, a.max_cpp, a.max_ppp);
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.max_cpp);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
         case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
@@ -2998,23 +2918,19 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int fused, int max_cpp, int max_ppp) {
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem) {
     hipError_t err = hipSuccess;
-    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, fused, max_cpp, max_ppp);
+    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, max_cpp);
     if (shmem > 64 * 1024) {
-#define SETA(M, R, P, F) hipFuncSetAttribute((const void*)&k_linearize<M, R, P, F>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
-        for (hipError_t e : {SETA(0, false, false, true), SETA(0, true, false, true), SETA(0, false, true, true),
-                             SETA(0, true, true, true), SETA(1, false, false, true), SETA(2, false, false, true),
-                             SETA(2, true, false, true), SETA(2, false, true, true), SETA(2, true, true, true),
-                             SETA(0, false, false, false), SETA(0, true, false, false), SETA(0, false, true, false),
-                             SETA(0, true, true, false), SETA(1, false, false, false), SETA(2, false, false, false),
-                             SETA(2, true, false, false), SETA(2, false, true, false), SETA(2, true, true, false)})
+#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
+        for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
+                             SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true),
+                             SETA(2, true, true)})
             if (e != hipSuccess) err = e;
 #undef SETA
     }
-    const size_t ps = mcc_photo_shmem(max_epp, max_ppp);
-    if (ps > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ps);
+    if (photo_shmem > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)photo_shmem);
         if (e != hipSuccess) err = e;
     }
     const size_t ss = mcc_solve_shmem(m);
