@@ -615,9 +615,16 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
-    // small camera blocks: one kernel per Gauss-Newton step (MCC_FUSED=0 forces the k_schur path)
-    p->fused = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
-    if (const char* f = std::getenv("MCC_FUSED")) p->fused = p->fused && std::atoi(f) != 0;
+    // small camera blocks and at most two photo workgroups per CU (the fused kernel's occupancy):
+    // one kernel per Gauss-Newton step.  More photos than that run the fused kernel's serial
+    // per-photo chain in several rounds, and the split step is faster (config4, 1000 views:
+    // 43.3 vs 47.4 us; config2, 500 views: 38.2 vs 25.9 us).  MCC_FUSED=1 / 0 forces either.
+    int n_cu = 256;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
+    const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
+    p->fused = fusable && V <= 2 * n_cu;
+    if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
     if (!p->fused && p->max_epp > 64)
         return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));

@@ -2087,13 +2087,18 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
     }
     __syncthreads();
     SSTAMP(stp, 4, 0);
-    // task (block pair k, row i): the group's contributions summed in order (photo, then edge pair)
-    for (int t = tid; t < 6 * nq; t += 256) {
-        const int k = t / 6, i = t % 6;
+    // task (block pair k, row i, part h of H): the group's contributions c = h, h + H, ... (photo,
+    // then edge pair order) summed by each part, the H parts (consecutive lanes) combined by a
+    // fixed xor butterfly.  H > 1 only when the group has few block pairs (a one-block rig:
+    // DoubleSide, every edge pair of the group lands in one slot) so the threads stay busy.
+    int H = 1;
+    while (H < 32 && 6 * nq * 2 * H <= 256) H *= 2;
+    for (int t = tid; t < 6 * nq * H; t += 256) {
+        const int h = t % H, k = t / H / 6, i = (t / H) % 6;
         const int4 pq = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}
         const bool diag = (pq.z & 2) != 0;
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, racc = 0.0, jacc = 0.0;
-        for (int c = pq.x; c < pq.x + pq.y; ++c) {
+        for (int c = pq.x + h; c < pq.x + pq.y; c += H) {
             const unsigned w = scn[c];
             const int ea = w & 255, eb = (w >> 8) & 255, q = w >> 17;
             const bool self = (w >> 16) & 1;
@@ -2126,12 +2131,20 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
                 jacc += gg;
             }
         }
-        double* out = a.pairprod + (size_t)pq.w;
+        for (int o = 1; o < H; o <<= 1) {   // the H parts are lanes t - h .. t - h + H - 1 (H | 64)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) out[i * 6 + j] = acc[j];
-        if (diag) {
-            out[36 + i] = racc;
-            out[42 + i] = jacc;
+            for (int j = 0; j < 6; ++j) acc[j] += __shfl_xor(acc[j], o);
+            racc += __shfl_xor(racc, o);
+            jacc += __shfl_xor(jacc, o);
+        }
+        if (h == 0) {
+            double* out = a.pairprod + (size_t)pq.w;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) out[i * 6 + j] = acc[j];
+            if (diag) {
+                out[36 + i] = racc;
+                out[42 + i] = jacc;
+            }
         }
     }
 #ifdef MCC_DIAG
