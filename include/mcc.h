@@ -152,12 +152,14 @@ int mcc_peer_enable(mcc_problem *p, int on);
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
 /* average device time (ms) per launch of the linearisation kernel over the last
  * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches.
- * Fused single-GPU problems (m <= 30: one kernel per step) time the whole window of graph-
- * launched steps with two events; others record an event pair around every launch (eager). */
+ * Fused single-GPU problems (m <= 30 and at most two photos per CU: one kernel per step) time
+ * the whole window of graph-launched steps with two events; split-step problems record an event
+ * pair around the k_prep + k_edge + k_photo launches of every step (eager). */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
 /* diagnostic build only (libmcc_diag.so, -DMCC_DIAG): first call arms per-phase s_memtime
- * stamps of k_linearize, later calls copy [32 * n_photos] stamps (then k_schur's [8 * grid]) out
+ * stamps (k_linearize; split step: k_photo per group, k_prep, k_edge rows), later calls copy
+ * [32 * n_photos] stamps (then k_schur's [8 * grid]) out
  * (others: MCC_EINVAL) */
 int mcc_debug_stamps(mcc_problem *p, long long *out, int n);
 /* static facts about the problem for roofline accounting */

@@ -21,7 +21,7 @@ CASES = {
     "config2_small": lambda: rig.make_config("config2", n_views=40),
     # DoubleSide (m = 6), fused
     "config5_small": lambda: rig.make_config("config5", n_views=24),
-    # m = 90: k_linearize + k_schur, the exchange runs in k_solve
+    # m = 90: the split step (k_prep, k_edge, k_photo, k_schur), the exchange runs in k_solve
     "config3_small": lambda: rig.make_config("config3", n_views=48),
     # a shard without any observation of one camera (config2, 40 views, camera 3 on rank 0 only)
     "config2_nocam": lambda: rig.make_config("config2", n_views=40),
