@@ -2218,6 +2218,10 @@ __device__ __forceinline__ int packed_index(int i, int j, int m) {   // i <= j
 // S is SPD: no pivoting.  x ends as the solution.
 typedef double v4f64_t __attribute__((ext_vector_type(4)));
 constexpr int kBlkLd = 17;   // stride of the 16 x 16 pivot-inverse scratch
+#ifndef MCC_SOLVE_THREADS
+#define MCC_SOLVE_THREADS 512
+#endif
+constexpr int kSolveThreads = MCC_SOLVE_THREADS;   // k_solve's workgroup for m > 30
 __device__ __forceinline__ int gjb_ld(int m) { return 16 * ((m + 15) / 16) + 1; }
 __device__ __forceinline__ void blk_mfma(double* C, int ldc, const double* Ap, int lda, const double* Bp, int ldb,
                                          bool sub, bool zero_c) {
@@ -2236,11 +2240,8 @@ __device__ __forceinline__ void blk_mfma(double* C, int ldc, const double* Ap, i
 #pragma unroll
     for (int r = 0; r < 4; ++r) C[(kq + 4 * r) * ldc + i] = acc[r];   // C[row = kq + 4r][col = i]
 }
-// 16 x 16 SPD inverse by one wave, all 64 lanes: lane l holds row i = l & 15, columns 8g .. 8g+7
-// (g = l >> 4) of [P | I].  Pivot k: its value by v_readlane, the pivot row's columns of every
-// lane by DPP row_newbcast:k inside each 16-lane row (the lanes of one column group), the
-// eliminated column entry of each row by one bpermute.  Columns left of the pivot in the P half are
-// left stale (never read).  Writes P^-1 to PV (stride kBlkLd); returns false if a pivot is not > 0.
+// 16 x 16 SPD inverse by one wave, all 64 lanes (GjbStep below).  Writes P^-1 to PV (stride
+// kBlkLd); returns false if a pivot is not > 0.
 template <int K>
 __device__ __forceinline__ double gjb_bcast16(double v) {
     const long long u = __double_as_longlong(v);
@@ -2249,48 +2250,54 @@ __device__ __forceinline__ double gjb_bcast16(double v) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + K, 0xF, 0xF, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// In-place Gauss-Jordan inversion (no identity half): lane l holds row i = l & 15, columns
+// 4g .. 4g+3 (g = l >> 4).  Pivot K: p = A[K][K] by v_readlane, ip = 1/p; the pivot row's columns of
+// every lane by DPP row_newbcast:K inside each 16-lane row (the lanes of one column group), A[i][K]
+// of each row by one bpermute; then A[i][j] -= f A[K][j] with f = A[i][K] ip, the pivot row is
+// scaled by ip, and column K becomes -f (ip on the diagonal).
 template <int K>
 struct GjbStep {
-    __device__ __forceinline__ static void run(double (&v)[8], int lane, double& dii, bool& ok) {
-        constexpr int gk = K >> 3, ck = K & 7;
+    __device__ __forceinline__ static void run(double (&v)[4], int lane, bool& ok) {
+        constexpr int gk = K >> 2, ck = K & 3;
         const double piv = readlane_f64(v[ck], K + 16 * gk);
         ok &= piv > 0.0;
         const double pv = piv > 0.0 ? piv : 1.0;
         double ip = __builtin_amdgcn_rcp(pv);
         ip = fma(ip, fma(-pv, ip, 1.0), ip);
-        const int i = lane & 15;
+        const int i = lane & 15, g = lane >> 4;
         const double rik = __shfl(v[ck], i + 16 * gk);   // row i's column-K entry
-        const double f = i == K ? 0.0 : rik * ip;
-        if (i == K) dii = pv;
-        double pr[8];
+        const bool prow = i == K;
+        // other rows: v - f pr with f = A[i][K] ip; the pivot row (pr = its own v): fma(ip, v, 0), an
+        // exactly rounded v ip (1 - ip and a difference would cancel when ip is tiny)
+        const double f = prow ? -ip : rik * ip;
+        const double keep = prow ? 0.0 : 1.0;
+        double pr[4];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) pr[c] = gjb_bcast16<K>(v[c]);
+        for (int c = 0; c < 4; ++c) pr[c] = gjb_bcast16<K>(v[c]);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) v[c] -= f * pr[c];
-        GjbStep<K + 1>::run(v, lane, dii, ok);
+        for (int c = 0; c < 4; ++c) v[c] = fma(-f, pr[c], v[c] * keep);
+        if (g == gk) v[ck] = prow ? ip : -f;
+        GjbStep<K + 1>::run(v, lane, ok);
     }
 };
 template <>
 struct GjbStep<16> {
-    __device__ __forceinline__ static void run(double (&)[8], int, double&, bool&) {}
+    __device__ __forceinline__ static void run(double (&)[4], int, bool&) {}
 };
+__device__ __forceinline__ bool gjb_inverse16_regs(double (&v)[4], double* PV, int lane) {
+    const int i = lane & 15, g = lane >> 4;
+    bool ok = true;
+    GjbStep<0>::run(v, lane, ok);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) PV[i * kBlkLd + 4 * g + c] = v[c];
+    return ok;
+}
 __device__ __forceinline__ bool gjb_inverse16(const double* Pk, int ld, double* PV, int lane) {
     const int i = lane & 15, g = lane >> 4;
-    double v[8];
+    double v[4];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const int col = 8 * g + c;
-        v[c] = col < 16 ? Pk[i * ld + (col < 16 ? col : 0)] : (col - 16 == i ? 1.0 : 0.0);
-    }
-    double dii = 1.0;
-    bool ok = true;
-    GjbStep<0>::run(v, lane, dii, ok);
-    if (g >= 2) {
-        const double id = 1.0 / dii;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) PV[i * kBlkLd + 8 * (g - 2) + c] = v[c] * id;
-    }
-    return ok;
+    for (int c = 0; c < 4; ++c) v[c] = Pk[i * ld + 4 * g + c];
+    return gjb_inverse16_regs(v, PV, lane);
 }
 #ifdef MCC_GJB_STAMPS
 __device__ long long g_gjb_stamps[64];
@@ -2307,47 +2314,59 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
     // (eight 16-B loads in flight, one memory round trip up to m = 90); the row of the first from
     // the quadratic's root with a one-step fix-up, the rest by stepping along the row; (i, j) and
     // (j, i) written
+    // Wave 0 meanwhile gathers the first pivot block (rows / columns 0..15, inside the matrix since
+    // m > 30) straight from the packed system and inverts it, off the load's critical path.
     const int nt = m * (m + 1) / 2;
     constexpr int PB = 16;
-    for (int t0 = PB * tid; t0 < nt; t0 += PB * (int)blockDim.x) {
-        double v[PB];
-        if (t0 + PB <= nt) {
-            const double2* p2 = reinterpret_cast<const double2*>(packed + t0);   // t0 even: 16-B aligned
+    bool bad = false;
+    if (wave == 0) {
+        const int i = lane & 15, g = lane >> 4;
+        double v0[4];
 #pragma unroll
-            for (int u = 0; u < PB / 2; ++u) { const double2 w = p2[u]; v[2 * u] = w.x; v[2 * u + 1] = w.y; }
-        } else {
-#pragma unroll
-            for (int u = 0; u < PB; ++u) v[u] = packed[min(t0 + u, nt - 1)];
+        for (int c = 0; c < 4; ++c) {
+            const int col = 4 * g + c;
+            v0[c] = packed[i <= col ? packed_index(i, col, m) : packed_index(col, i, m)];
         }
-        const double b = 2.0 * m + 1.0;
-        int i = (int)((b - sqrt(b * b - 8.0 * t0)) * 0.5);
-        i = max(0, min(i, m - 1));
-        if (packed_index(i, i, m) > t0) --i;
-        else if (i + 1 < m && packed_index(i + 1, i + 1, m) <= t0) ++i;
-        int j = i + (t0 - packed_index(i, i, m));
+        bad |= !gjb_inverse16_regs(v0, PV, lane);
+    } else {
+        const int lt = tid - 64, nlt = (int)blockDim.x - 64;
+        for (int t0 = PB * lt; t0 < nt; t0 += PB * nlt) {
+            double v[PB];
+            if (t0 + PB <= nt) {
+                const double2* p2 = reinterpret_cast<const double2*>(packed + t0);   // t0 even: 16-B aligned
 #pragma unroll
-        for (int u = 0; u < PB; ++u) {
-            if (t0 + u < nt) {
-                A[i * ld + j] = v[u];
-                A[j * ld + i] = v[u];
+                for (int u = 0; u < PB / 2; ++u) { const double2 w = p2[u]; v[2 * u] = w.x; v[2 * u + 1] = w.y; }
+            } else {
+#pragma unroll
+                for (int u = 0; u < PB; ++u) v[u] = packed[min(t0 + u, nt - 1)];
             }
-            if (++j == m) { ++i; j = i; }
+            const double b = 2.0 * m + 1.0;
+            int i = (int)((b - sqrt(b * b - 8.0 * t0)) * 0.5);
+            i = max(0, min(i, m - 1));
+            if (packed_index(i, i, m) > t0) --i;
+            else if (i + 1 < m && packed_index(i + 1, i + 1, m) <= t0) ++i;
+            int j = i + (t0 - packed_index(i, i, m));
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+                if (t0 + u < nt) {
+                    A[i * ld + j] = v[u];
+                    A[j * ld + i] = v[u];
+                }
+                if (++j == m) { ++i; j = i; }
+            }
         }
+        // padding: rows m .. M-1 (every column) and columns m .. M-1 of rows < m
+        for (int i = m + wave - 1; i < M; i += nw - 1)
+            for (int j = lane; j < M; j += 64) A[i * ld + j] = i == j ? 1.0 : 0.0;
+        for (int i = lt; i < m; i += nlt)
+            for (int j = m; j < M; ++j) A[i * ld + j] = 0.0;
     }
-    // padding: rows m .. M-1 (every column) and columns m .. M-1 of rows < m
-    for (int i = m + wave; i < M; i += nw)
-        for (int j = lane; j < M; j += 64) A[i * ld + j] = i == j ? 1.0 : 0.0;
-    for (int i = tid; i < m; i += blockDim.x)
-        for (int j = m; j < M; ++j) A[i * ld + j] = 0.0;
     if (tid < M) x[tid] = xr;
     __syncthreads();
     GJB_STAMP(0);
-    bool bad = false;
-    // (1) pivot block inverse of block 0; later pivots are inverted one step ahead (look-ahead):
-    // in step kb, wave 0 first eliminates block (kb+1, kb+1) and inverts it while waves 1..3
-    // eliminate the rest; PV holds two 16 x 17 buffers (step parity)
-    if (wave == 0) bad |= !gjb_inverse16(A, ld, PV, lane);
-    __syncthreads();
+    // later pivots are inverted one step ahead (look-ahead): in step kb, wave 0 first eliminates
+    // block (kb+1, kb+1) and inverts it while the other waves eliminate the rest; PV holds two
+    // 16 x 17 buffers (step parity)
     for (int kb = 0; kb < nb; ++kb) {
         GJB_STAMP(1 + 3 * kb);
         const double* PVk = PV + (kb & 1) * 16 * kBlkLd;
@@ -2623,7 +2642,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
 }
 
 // ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)
-__global__ __launch_bounds__(256) void k_solve(SolveArgs a) {
+__global__ __launch_bounds__(1024) void k_solve(SolveArgs a) {
     if (a.ctx.state->done) return;
     const int m = a.ctx.m, tid = threadIdx.x, ntri = m * (m + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -2964,7 +2983,9 @@ hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), mcc_solve_shmem(a.ctx.m), s, a);
+    // m > 30: 8 waves, so the block eliminations of a pivot step (up to (nb - 1)^2 16 x 16 MFMA
+    // products) are not what waits on the next pivot inverse
+    hipLaunchKernelGGL(k_solve, dim3(1), dim3(a.ctx.m > 30 ? kSolveThreads : 256), mcc_solve_shmem(a.ctx.m), s, a);
     return hipGetLastError();
 }
 hipError_t mcc_launch_peer_handshake(const PeerCtx& pc, State* st, double* out, hipStream_t s) {

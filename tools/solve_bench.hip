@@ -1,5 +1,5 @@
 // Micro-benchmark of the large-m reduced-system elimination (gj_blocked, m > 30) in isolation.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/solve_bench.hip -o tools/solve_bench -lrccl && tools/solve_bench [m]
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/solve_bench.hip -o tools/solve_bench -lrccl && tools/solve_bench [m] [threads]
 // One 256-thread workgroup solves a random SPD packed system REPS times; prints the median
 // s_memtime ticks per solve and the max relative error against a host Cholesky solve.
 #ifndef MCC_GJB_STAMPS
@@ -14,7 +14,7 @@
 
 constexpr int REPS = 16;
 
-__global__ void k_solve_bench(const double* packed, int m, double* xout, long long* ticks, int* err) {
+__global__ __launch_bounds__(1024) void k_solve_bench(const double* packed, int m, double* xout, long long* ticks, int* err) {
     extern __shared__ double smb[];
     const int M = 16 * ((m + 15) / 16);
     double* x = smb;
@@ -34,6 +34,7 @@ __global__ void k_solve_bench(const double* packed, int m, double* xout, long lo
 
 int main(int argc, char** argv) {
     const int m = argc > 1 ? std::atoi(argv[1]) : 90;
+    const int nt = argc > 2 ? std::atoi(argv[2]) : 256;   // workgroup size
     std::mt19937_64 rng(11);
     std::normal_distribution<double> nd;
     std::vector<double> B(m * m), S(m * m, 0.0), r(m);
@@ -80,10 +81,10 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL(k_solve_bench, dim3(1), dim3(256), shm, 0, dp, m, dx, dt, de);   // warm-up
+    hipLaunchKernelGGL(k_solve_bench, dim3(1), dim3(nt), shm, 0, dp, m, dx, dt, de);   // warm-up
     (void)hipDeviceSynchronize();
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL(k_solve_bench, dim3(1), dim3(256), shm, 0, dp, m, dx, dt, de);
+    hipLaunchKernelGGL(k_solve_bench, dim3(1), dim3(nt), shm, 0, dp, m, dx, dt, de);
     (void)hipEventRecord(e1, 0);
     hipError_t e = hipDeviceSynchronize();
     float ms = 0.f;
