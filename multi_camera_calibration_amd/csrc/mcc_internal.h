@@ -115,7 +115,7 @@ __host__ __device__ inline size_t photo_lds_bytes(int gne, int npairs, int ncon)
 struct SchurArgs {
     State* state;
     const int4* items;   // {camera-pair block, first slot's offset in doubles, slot count, slot size 48 | 36}
-    const double* pairprod;   // 48 (diagonal block) or 36 doubles per pair, written by k_linearize, block-major
+    const double* pairprod;   // 48 (diagonal block) or 36 doubles per slot, written by k_photo, block-major
     double* item_out;    // [48 * (items + norm chunks)]
     int n_items;
     const double* photo_norm; int n_photos;

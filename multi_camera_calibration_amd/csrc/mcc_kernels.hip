@@ -2511,10 +2511,10 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 
 // ---------------------------------------------------------------- k_schur
 // Work item {block, offset of its first slot in doubles, slot count, slot size 48 | 36}: a run of
-// consecutive slots of one camera-pair block.  k_linearize wrote each pair's product
-// at its slot (48 doubles: [self] Hgg_a - Y'_a Hgp_b^T, [self] (gg_a - Y'_a gp), [self] gg_a; 36 on an
-// off-diagonal block, which has no self pair), so an
-// item streams and sums them.  Thread t < 240: entry q = t % 48 (0..35: S entry, 36..41: r entry,
+// consecutive slots of one camera-pair block.  k_photo wrote one slot per (photo group, block):
+// the group's sum of the block's pair products (48 doubles: sum of [self] Hgg_a - Y'_a Hgp_b^T,
+// [self] (gg_a - Y'_a gp), [self] gg_a; 36 on an off-diagonal block, which has no self pair), so
+// an item streams and sums them.  Thread t < 240: entry q = t % 48 (0..35: S entry, 36..41: r entry,
 // 42..47: JTE of the global block), sub-chunk s = t / 48.
 // Norm items sum 256 photos' norm partials.  Hand-off in two write-through levels (sc1 stores,
 // tickets, no fences): the last item of each camera-pair block sums the block's items in item
@@ -2536,7 +2536,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         const int q = tid % 48, sub = tid / 48, sz = it.w;
         double s = 0.0;
         if (sub < kSub) {
-            // the products k_linearize wrote at the block's slots: independent coalesced loads,
+            // the group sums k_photo wrote at the block's slots: independent coalesced loads,
             // eight in flight per thread (entries >= 36 of an off-diagonal block: none, zeros)
             if (q < sz) {
                 // slots sub, sub + kSub, ... summed in that order; 24 loads per thread in flight per
