@@ -1447,20 +1447,11 @@ constexpr int kMaxEdgesPerPhoto = 64;   // split step (k_prep's LDS; mcc_create 
 #define MCC_PREP_WAVES 2           // k_prep waves per SIMD
 #endif
 // camera vertex c's pose (om, T): DoubleSide's fixed cameras, camera 0 = identity, else x
-template <int MODEL>
-__device__ __forceinline__ void camera_pose(const LinArgs& a, int cam, double* om2, double* T2) {
+__device__ __forceinline__ void camera_pose_lds(const double* cam6, int cam, double* om2, double* T2) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        if (MODEL == MCC_MODEL_DOUBLESIDE) {
-            om2[k] = a.cam_rt[6 * cam + k];
-            T2[k] = a.cam_rt[6 * cam + 3 + k];
-        } else if (cam == 0) {   // src/mymulticalib.cpp:721-725
-            om2[k] = 0.0;
-            T2[k] = 0.0;
-        } else {
-            om2[k] = a.x[6 * (cam - 1) + k];
-            T2[k] = a.x[6 * (cam - 1) + 3 + k];
-        }
+        om2[k] = cam6[6 * cam + k];
+        T2[k] = cam6[6 * cam + 3 + k];
     }
 }
 // BACK: the problem has back-side edges (MyMulti doubleSideTransform / DoubleSide), so the
@@ -1476,11 +1467,22 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     __shared__ double s_v[64 / kPrepGroup][16];
     __shared__ double s_part[64 / kPrepGroup][kMaxEdgesPerPhoto][6];
     __shared__ double s_ph[64 / kPrepGroup][44];   // R1, Jr1, T1, Rds, Jrds, dst (the group's photo)
+    // camera poses (rvec, tvec per camera), the previous step's dg and the double-side transform,
+    // staged in the first round trip with the photo ranges (no dependent load for them later)
+    __shared__ double s_cam[6 * 64], s_dg[128], s_ds[6];   // <= 63 cameras, m <= 128 (mcc_create)
     const bool valid = photo < a.n_photos;
     const int e0 = valid ? a.photo_ptr[photo] : 0;
     const int ne = valid ? a.photo_ptr[photo + 1] - e0 : 0;
     const int pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update
+    for (int q = tid; q < 6 * a.n_cams; q += 64) {
+        const int c = q / 6, k = q % 6;
+        s_cam[q] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.cam_rt[q]
+                                                 : (c == 0 ? 0.0 : (double)a.x[6 * (c - 1) + k]);   // src/mymulticalib.cpp:721-725
+    }
+    for (int q = tid; q < a.global_dim; q += 64) s_dg[q] = a.dg[q];
+    if (BACK && tid < 6) s_ds[tid] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[tid] : a.ds_rt[tid];
+    wave_sync_lds();
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
     // the camera of the lane's first edge: Rodrigues + Jl, independent of the photo update
     int4 info0 = make_int4(0, 0, 0, 0);
@@ -1489,7 +1491,7 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     if (l < ne) {
         info0 = a.edge_info[e0 + l];
         double om2[3];
-        camera_pose<MODEL>(a, info0.x, om2, T2);
+        camera_pose_lds(s_cam, info0.x, om2, T2);
         rodrigues_v2m(om2, r2);
         so3_jac(om2, r2, +1.0, Jl2);
     }
@@ -1510,7 +1512,7 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
             double y[36];
 #pragma unroll
             for (int q = 0; q < 36; ++q) y[q] = Ye[q];
-            const double* d = a.dg + 6 * (g < 0 ? 0 : g);
+            const double* d = s_dg + 6 * (g < 0 ? 0 : g);
             double dv[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) dv[i] = d[i];
@@ -1568,8 +1570,8 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
         double dsr[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            dsr[k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[k] : a.ds_rt[k];
-            ph[39 + k] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[3 + k] : a.ds_rt[3 + k];
+            dsr[k] = s_ds[k];
+            ph[39 + k] = s_ds[3 + k];
         }
         Rot rd;
         rodrigues_v2m(dsr, rd);
@@ -1586,7 +1588,7 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
         if (le >= kPrepGroup) {   // more than 16 edges: this edge's camera
             info = a.edge_info[e];
             double om2[3];
-            camera_pose<MODEL>(a, info.x, om2, T2);
+            camera_pose_lds(s_cam, info.x, om2, T2);
             rodrigues_v2m(om2, r2);
             so3_jac(om2, r2, +1.0, Jl2);
         }
