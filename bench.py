@@ -199,7 +199,8 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
            "model": {rig.PINHOLE: "pinhole", rig.OMNI: "omnidir", rig.DOUBLESIDE: "doubleside"}[p.model],
            "steps": steps, "ms_per_step": ms, "corner_evals_per_s": p.n_corners / (ms * 1e-3),
            "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
-           "roofline": roofline(st, m["lin_ms"], kernel=lin_kernels(p)), "rig_generation_s": round(gen_s, 2)}
+           "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=lin_kernels(p)),
+           "rig_generation_s": round(gen_s, 2)}
     fp = load_profile("fp64", name, p.n_photos)
     if fp and fp.get("fp64_flops_per_launch"):
         tf = fp["fp64_flops_per_launch"] / (m["lin_ms"] * 1e-3) / 1e12
