@@ -1091,9 +1091,9 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
                 for (int r = 0; r < 6; ++r)
 #pragma unroll
-                    for (int s = r; s < 6; ++s) acc[q++] += ju[r] * ju[s] + jv[r] * jv[s];
+                    for (int s = r; s < 6; ++s, ++q) acc[q] = fma(jv[r], jv[s], fma(ju[r], ju[s], acc[q]));
 #pragma unroll
-                for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
+                for (int r = 0; r < 6; ++r) acc[21 + r] = fma(jv[r], ev, fma(ju[r], eu, acc[21 + r]));
             }
             if (wave == 0) STAMP(3);
             const double sum = wave_reduce_scatter32(acc, lane);
@@ -1784,9 +1784,9 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
 #pragma unroll
             for (int r = 0; r < 6; ++r)
 #pragma unroll
-                for (int s2 = r; s2 < 6; ++s2) acc[q++] += ju[r] * ju[s2] + jv[r] * jv[s2];
+                for (int s2 = r; s2 < 6; ++s2, ++q) acc[q] = fma(jv[r], jv[s2], fma(ju[r], ju[s2], acc[q]));
 #pragma unroll
-            for (int r = 0; r < 6; ++r) acc[21 + r] += ju[r] * eu + jv[r] * ev;
+            for (int r = 0; r < 6; ++r) acc[21 + r] = fma(jv[r], ev, fma(ju[r], eu, acc[21 + r]));
         }
     }
     SSTAMP(stp, 2, 0);
