@@ -1669,7 +1669,7 @@ constexpr int kEdgeChunk = 96;    // corners of one edge staged in LDS at a time
 #define MCC_EDGE_WAVES 4            // k_edge waves per SIMD (register budget 128 VGPRs)
 #endif
 template <int MODEL, bool RATIONAL, bool PRISM, int L>
-__global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
+__global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) ? 3 : MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     if (a.state->done) return;
     constexpr int GPB = 64 / L;   // edges per workgroup (one wave)
     const int tid = threadIdx.x, g = tid / L, sub = tid % L;
@@ -1682,13 +1682,18 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     struct Chain { double A[36], B[6], G[72], X[72]; };
     __shared__ __attribute__((aligned(16))) union { float C[GPB][5][kEdgeChunk]; Chain H[GPB]; } sU;
     __shared__ double sP[GPB][30];
+    __shared__ int sI[GPB][2];   // corner offset and count, re-read per chunk (nothing stays live through the sweep)
     auto& sC = sU.C;
     if (e >= a.n_edges) return;   // whole groups: L divides the wave
     const int4 info = a.edge_info[e];
     const int cam = info.x, off = info.z, n = info.w;
+    if (sub == 0) {
+        sI[g][0] = off;
+        sI[g][1] = n;
+    }
     // the edge's corners (contiguous in all five streams) -> LDS, every load in flight at once;
     // chain maps (consumed after the sweep) expanded into Gp, Gg (6 x 6)
-    auto stage = [&](int c0, int cn) {   // every load of the chunk issued before the first LDS store
+    auto stage = [&](int eoff, int c0, int cn) {   // every load of the chunk issued before the first LDS store
         constexpr int PER = kEdgeChunk / L;
         float v[PER][5];
         int sb = sub;   // opaque: the lane's chunk offsets are recomputed per chunk, not kept live (spilled)
@@ -1698,7 +1703,7 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
             const int i = sb + L * u;
             // 32-bit element index: SGPR base + one VGPR offset per load (saddr form), not a 64-bit
             // address pair per stream, which spilled to scratch
-            const unsigned c = (unsigned)(off + c0 + (i < cn ? i : 0));
+            const unsigned c = (unsigned)(eoff + c0 + (i < cn ? i : 0));
             v[u][0] = a.obj_x[c];
             v[u][1] = a.obj_y[c];
             v[u][2] = a.obj_z[c];
@@ -1714,7 +1719,7 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
             }
         }
     };
-    stage(0, min(n, kEdgeChunk));
+    stage(off, 0, min(n, kEdgeChunk));
     SSTAMP(stp, 1, 0);
     // the edge's pose and camera (R, T, fx, fy, cx, cy, skew, xi, k[12]) in LDS, re-read by every
     // corner (an opaque offset keeps the compiler from hoisting them into ~50 more VGPRs, which
@@ -1736,11 +1741,14 @@ __global__ __launch_bounds__(64, MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     double acc[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) acc[q] = 0.0;
-    for (int c0 = 0; c0 < n; c0 += kEdgeChunk) {
-        const int cn = min(n - c0, kEdgeChunk);
+    wave_sync_lds();
+    for (int c0 = 0;; c0 += kEdgeChunk) {
+        const int nn = sI[g][1];
+        if (c0 >= nn) break;
+        const int cn = min(nn - c0, kEdgeChunk);
         if (c0 > 0) {
             wave_sync_lds();   // the previous chunk is consumed
-            stage(c0, cn);
+            stage(sI[g][0], c0, cn);
         }
         wave_sync_lds();
 #pragma unroll 1

@@ -2,7 +2,7 @@
 # One GPU-box pass (run from the repo root through gpurun):
 #   1. the -m gpu test suite (every test, failures listed; a crash / timeout stops the script)
 #   2. bench.py at the driver's settings (--steps 20 --warmup 5) and at its defaults
-#   3. rocprofv3 --kernel-trace --stats of the driver-settings bench (all configs' kernels)
+#   3. rocprofv3 --kernel-trace --stats of the driver-settings bench, one process per config
 # Usage: tools/gpu_round.sh <tag> [tests|bench|prof ...]   (default: all three)
 set -o pipefail
 TAG=${1:-r02}
@@ -33,11 +33,20 @@ for s in $STEPS; do
         echo "bench (defaults):"; cut -c1-400 "$OUT/bench_default.json"
         ;;
     prof)
-        ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run \
-            --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu --no-parity \
-            > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" ) || exit 13
-        f=$(find "$OUT/stats" -name "*kernel_stats.csv" | head -n 1)
-        [ -n "$f" ] && cp "$f" "$OUT/kernel_stats.csv" && cut -c1-160 "$OUT/kernel_stats.csv"
+        # one process per config (--no-extra), and config4 with eager launches (MCC_GRAPH=0): under
+        # rocprofv3 --kernel-trace, graph-launched split steps abort in two reproducible cases --
+        # HSA_STATUS_ERROR_INVALID_PACKET_FORMAT when they follow the fused step's graphs in the
+        # same process (config2 then config3), and a host SIGSEGV inside hipGraphLaunch for the
+        # m = 18 split step (config4; config2 with MCC_FUSED=0).  Eager launches, m = 6 / 90 split
+        # steps alone, and every run without the profiler are fine (tools/repro_prof.sh).
+        for cfg in config2 config3 config4 config5; do
+            g=1; [ $cfg = config4 ] && g=0
+            ( cd /tmp && export TMPDIR=/tmp && export MCC_GRAPH=$g && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run \
+                --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu --no-parity --no-extra \
+                > "$OUT/prof_$cfg.json" 2> "$OUT/prof_$cfg.err" ) || exit 13
+            f=$(find "$OUT/stats_$cfg" -name "*kernel_stats.csv" | head -n 1)
+            [ -n "$f" ] && cp "$f" "$OUT/kernel_stats_$cfg.csv" && echo "== $cfg" && cut -c1-120 "$OUT/kernel_stats_$cfg.csv" | grep k_
+        done
         ;;
     esac
 done
