@@ -2549,10 +2549,10 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             // the group sums k_photo wrote at the block's slots: independent coalesced loads,
             // eight in flight per thread (entries >= 36 of an off-diagonal block: none, zeros)
             if (q < sz) {
-                // slots sub, sub + kSub, ... summed in that order; 24 loads per thread in flight per
-                // round (one round for the ~100-slot items of a 5k-view rig)
+                // slots sub, sub + kSub, ... summed in that order; 32 loads per thread in flight per
+                // round (one round for the host's items of <= 160 slots)
                 const double* pp = a.pairprod + (size_t)it.y + q;
-                constexpr int U = 24;
+                constexpr int U = 32;
                 for (int p0 = sub; p0 < it.z; p0 += U * kSub) {
                     double v[U];
 #pragma unroll
