@@ -159,11 +159,10 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
                 ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)})
 
 
-def lin_kernels(p) -> str:
-    """The kernels of the linearisation window (mcc_timing_*): one fused kernel for m <= 30, the
-    split step's three for m > 30."""
-    m = 6 if p.model == rig.DOUBLESIDE else 6 * (p.n_cams - 1)
-    return "k_prep+k_edge+k_photo" if m > 30 else "k_linearize"
+def lin_kernels(ba) -> str:
+    """The kernels of the linearisation window (mcc_timing_*): the fused kernel, or the split
+    step's three (mcc_problem_path says which the problem runs)."""
+    return "k_prep+k_edge+k_photo" if ba.path() == "split" else "k_linearize"
 
 
 def roofline(st, lin_ms, tr=None, kernel="k_linearize"):
@@ -192,6 +191,7 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
         ba.set_params(p.x0)
         m = measure(ba, steps, warmup, 0.15, max(100, steps))
         st = ba.stats()
+        kern = lin_kernels(ba)
     finally:
         ba.close()
     ms = m["dt"] / steps * 1e3
@@ -199,7 +199,7 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
            "model": {rig.PINHOLE: "pinhole", rig.OMNI: "omnidir", rig.DOUBLESIDE: "doubleside"}[p.model],
            "steps": steps, "ms_per_step": ms, "corner_evals_per_s": p.n_corners / (ms * 1e-3),
            "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
-           "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=lin_kernels(p)),
+           "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=kern),
            "rig_generation_s": round(gen_s, 2)}
     fp = load_profile("fp64", name, p.n_photos)
     if fp and fp.get("fp64_flops_per_launch"):
@@ -305,6 +305,7 @@ def main():
 
     m = measure(ba, args.steps, args.warmup, args.ramp_seconds, max(100, args.steps))
     st = ba.stats()
+    kern = lin_kernels(ba)
     corners_total = float(full.n_corners)
     value = corners_total * args.steps / m["dt"]
     ms_per_step = m["dt"] / args.steps * 1e3
@@ -318,7 +319,7 @@ def main():
     if rank != 0:
         return
     tr = load_profile("traffic", args.config, views_per_rank) if world == 1 else None
-    rl = roofline(st, m["lin_ms"], tr, kernel=lin_kernels(prob))
+    rl = roofline(st, m["lin_ms"], tr, kernel=kern)
     rl["kernel_launches_timed"] = m["nlaunch"]
     rl["step_ms_events"] = m["step_ms_ev"]
     out = {

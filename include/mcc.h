@@ -165,6 +165,10 @@ int mcc_debug_stamps(mcc_problem *p, long long *out, int n);
 /* static facts about the problem for roofline accounting */
 int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges,
                       long long *photos, long long *alg_bytes_per_step);
+/* which step the problem runs: *split_step = 0 for the fused single-kernel step (m <= 30 and at
+ * most two photo workgroups per CU, or MCC_FUSED=1), 1 for the split step (k_prep, k_edge,
+ * k_photo, k_schur, k_solve); *photo_groups = k_photo's workgroups (split step) */
+int mcc_problem_path(const mcc_problem *p, int *split_step, int *photo_groups);
 
 #ifdef __cplusplus
 }

@@ -103,6 +103,7 @@ def lib():
         L.mcc_timing_begin.argtypes = [ctypes.c_void_p]
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
+        L.mcc_problem_path.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.mcc_comm_unique_id.argtypes = [ctypes.c_char_p]
         L.mcc_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.mcc_comm_allreduce_max.argtypes = [ctypes.c_void_p, _f64p]
@@ -294,6 +295,13 @@ class BundleAdjuster:
         v = [ctypes.c_longlong(0) for _ in range(4)]
         _check(lib().mcc_problem_stats(self.h, *[ctypes.byref(t) for t in v]), "mcc_problem_stats")
         return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
+
+    def path(self):
+        """'fused' (one kernel per step) or 'split' (k_prep, k_edge, k_photo, k_schur, k_solve)."""
+        sp = ctypes.c_int(0)
+        ng = ctypes.c_int(0)
+        _check(lib().mcc_problem_path(self.h, ctypes.byref(sp), ctypes.byref(ng)), "mcc_problem_path")
+        return "split" if sp.value else "fused"
 
     def stamps(self):
         """libmcc_diag.so only: first call arms, later calls return [n_photos, 32] s_memtime stamps

@@ -968,6 +968,13 @@ int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launche
     return MCC_OK;
 }
 
+int mcc_problem_path(const mcc_problem* p, int* split_step, int* photo_groups) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    if (split_step) *split_step = p->fused ? 0 : 1;
+    if (photo_groups) *photo_groups = p->fused ? 0 : p->n_pgroups;
+    return MCC_OK;
+}
+
 int mcc_problem_stats(const mcc_problem* p, long long* corners, long long* edges, long long* photos,
                       long long* alg_bytes) {
     if (!p) return fail(MCC_EINVAL, "null problem");

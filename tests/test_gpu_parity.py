@@ -249,3 +249,22 @@ def test_unobserved_camera_not_pd():
             g.compute_jacobian_extrinsic(q.x0)
     finally:
         g.close()
+
+
+def test_step_path_selection():
+    """mcc_create's choice (mcc_problem_path): the fused single-kernel step for m <= 30 with at most
+    two photo workgroups per CU, the split step for more photos or m > 30; MCC_FUSED=0 forces the
+    split step (the *_split cases above)."""
+    cases = [("config2", 500, "fused"), ("config2", 1200, "split"), ("config3", 40, "split"), ("config5", 60, "fused")]
+    for name, views, want in cases:
+        p = rig.make_config(name, n_views=views)
+        g = api.BundleAdjuster(p)
+        try:
+            assert g.path() == want, (name, views)
+        finally:
+            g.close()
+    g = make_adjuster("config2_small_split", rig.make_config("config2", n_views=30))
+    try:
+        assert g.path() == "split"
+    finally:
+        g.close()
