@@ -167,9 +167,13 @@ struct mcc_problem {
     State* h_state = nullptr;   // pinned staging
     int packed_len = 0, ntri = 0;
 
-    // graphs: [0] one update step, [1] kGraphSteps update steps
+    // graphs: gexec[k] = 2^k update steps (k < kGraphSizes), built on first use; a run of n steps
+    // is launched as the binary decomposition of n (20 steps: two launches, 16 + 4).
+    // mcc_optimize polls the device stop test every kGraphSteps steps.
     static constexpr int kGraphSteps = 8;
-    hipGraphExec_t gexec[2] = {nullptr, nullptr};
+    static constexpr int kGraphSizes = 7;   // up to 64 steps per launch
+    hipGraphExec_t gexec[kGraphSizes] = {};
+    int graph_sizes = kGraphSizes;   // MCC_GRAPH_SIZES (A/B of the launch granularity)
     bool use_graph = true;
     // the device State is in free-running mode (crit_type 0) since the last mcc_step: later
     // mcc_step calls enqueue without a host round trip (set_state clears it)
@@ -324,23 +328,19 @@ int enqueue_backsub(mcc_problem* p, int do_update) {
     return MCC_OK;
 }
 
-int build_graphs(mcc_problem* p) {
-    if (p->gexec[0]) return MCC_OK;
-    const int counts[2] = {1, mcc_problem::kGraphSteps};
-    for (int g = 0; g < 2; ++g) {
-        hipGraph_t graph;
-        HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
-        int rc = MCC_OK;
-        for (int s = 0; s < counts[g] && rc == MCC_OK; ++s) rc = enqueue_step(p, 1, nullptr);
-        hipError_t ee = hipStreamEndCapture(p->stream, &graph);
-        if (rc != MCC_OK) return rc;
-        if (ee != hipSuccess) return fail(MCC_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ee));
-        HIPCHK(hipGraphInstantiate(&p->gexec[g], graph, nullptr, nullptr, 0));
-        HIPCHK(hipGraphDestroy(graph));
-    }
+int build_graph(mcc_problem* p, int k) {
+    if (p->gexec[k]) return MCC_OK;
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+    int rc = MCC_OK;
+    for (int s = 0; s < (1 << k) && rc == MCC_OK; ++s) rc = enqueue_step(p, 1, nullptr);
+    hipError_t ee = hipStreamEndCapture(p->stream, &graph);
+    if (rc != MCC_OK) return rc;
+    if (ee != hipSuccess) return fail(MCC_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ee));
+    HIPCHK(hipGraphInstantiate(&p->gexec[k], graph, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(graph));
     return MCC_OK;
 }
-
 int launch_update_steps(mcc_problem* p, int n) {
     if (p->timing_window) p->win_steps += n;
     if (p->timing || !p->use_graph) {
@@ -350,13 +350,14 @@ int launch_update_steps(mcc_problem* p, int n) {
         }
         return MCC_OK;
     }
-    int rc = build_graphs(p);
-    if (rc) return rc;
-    while (n >= mcc_problem::kGraphSteps) {
-        HIPCHK(hipGraphLaunch(p->gexec[1], p->stream));
-        n -= mcc_problem::kGraphSteps;
+    for (int k = p->graph_sizes - 1; k >= 0; --k) {
+        while (n >= (1 << k)) {
+            int rc = build_graph(p, k);
+            if (rc) return rc;
+            HIPCHK(hipGraphLaunch(p->gexec[k], p->stream));
+            n -= 1 << k;
+        }
     }
-    while (n-- > 0) HIPCHK(hipGraphLaunch(p->gexec[0], p->stream));
     return MCC_OK;
 }
 
@@ -463,6 +464,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(hipSetDevice(d->device));
     HIPC(stream_pool().take(d->device, &p->stream));
     if (const char* g = std::getenv("MCC_GRAPH")) p->use_graph = std::atoi(g) != 0;
+    if (const char* g = std::getenv("MCC_GRAPH_SIZES"))
+        p->graph_sizes = std::min(mcc_problem::kGraphSizes, std::max(1, std::atoi(g)));
 
     // distortion specialisation (zero coefficients are exact no-ops in OpenCV's formula)
     if (d->model != MCC_MODEL_OMNI) {
