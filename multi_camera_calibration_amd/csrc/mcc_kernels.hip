@@ -1601,98 +1601,92 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     SSTAMP(stp, 3, 0);
 }
 
-// Reduce-scatter butterfly of 32 per-lane values over a group of L lanes (L = 16 or 8: one DPP
-// row or half of one), fixed order: afterwards lane sub holds the full group sums of value
-// indices base + q (q < 32 / L), base = sum over the group's lane bits d of (sub & d ? 16 d / L * ... )
-template <int L>
-__device__ __forceinline__ void group_reduce_scatter(double* v, int lane) {
-    static_assert(L == 16 || L == 8, "group size");
-    int c = 32;
-    if (L == 16) {   // xor 8: rotate a row by 8
+// Reduce-scatter of 32 per-lane values over the 16 lanes {g, g + 4, ..., g + 60} of one edge
+// (k_edge's strided lane map, g = lane & 3): xor 32 and 16 as whole half-wave / row swaps
+// (v_permlane32_swap, v_permlane16_swap: two instructions and an add per value pair instead of
+// selects around DPP), xor 8 and 4 by DPP inside a row.  In the edge's own numbering
+// (sub = lane >> 2) this is the fixed tree sub ^ 8, ^ 4, ^ 2, ^ 1.  Afterwards the lane holds the
+// edge's sums of value indices strided_rs_base(lane) + {0, 1}.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64u(double v) {   // no 'old' operand to initialise
+    const unsigned long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
+    return ull_f64((unsigned)lo, (unsigned)hi);
+}
+__device__ __forceinline__ void strided_reduce_scatter16(double* v, int lane) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { double p = v[j], q = v[j + 16]; pl32_swap(p, q); v[j] = p + q; }   // sub ^ 8
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { double p = v[j], q = v[j + 8]; pl16_swap(p, q); v[j] = p + q; }     // sub ^ 4
+    {   // sub ^ 2 = lane ^ 8: rotate a row by 8
         const bool hi = (lane & 8) != 0;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const double send = hi ? v[j] : v[j + 16], keep = hi ? v[j + 16] : v[j];
-            v[j] = keep + dpp_f64<kDppRor8>(send);
+        for (int j = 0; j < 4; ++j) {
+            const double send = hi ? v[j] : v[j + 4], keep = hi ? v[j + 4] : v[j];
+            v[j] = keep + dpp_f64u<kDppRor8>(send);
         }
-        c = 16;
     }
-    {   // xor 4: i - 4 for the upper, i + 4 = i - 12 for the lower
+    {   // sub ^ 1 = lane ^ 4: i - 4 for the upper, i + 4 = i - 12 for the lower
         const bool hi = (lane & 4) != 0;
-        const int h = c / 2;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if (j >= h) break;
-            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
-            const double p4 = dpp_f64<kDppRor4>(send), p12 = dpp_f64<kDppRor12>(send);
+        for (int j = 0; j < 2; ++j) {
+            const double send = hi ? v[j] : v[j + 2], keep = hi ? v[j + 2] : v[j];
+            const double p4 = dpp_f64u<kDppRor4>(send), p12 = dpp_f64u<kDppRor12>(send);
             v[j] = keep + (hi ? p4 : p12);
         }
-        c = h;
-    }
-    {   // xor 2
-        const bool hi = (lane & 2) != 0;
-        const int h = c / 2;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if (j >= h) break;
-            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
-            v[j] = keep + dpp_f64<kDppXor2>(send);
-        }
-        c = h;
-    }
-    {   // xor 1
-        const bool hi = (lane & 1) != 0;
-        const int h = c / 2;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (j >= h) break;
-            const double send = hi ? v[j] : v[j + h], keep = hi ? v[j + h] : v[j];
-            v[j] = keep + dpp_f64<kDppXor1>(send);
-        }
     }
 }
-// first value index a lane holds after group_reduce_scatter<L>
-template <int L>
-__device__ __forceinline__ int group_rs_base(int lane) {
-    return L == 16 ? 16 * ((lane >> 3) & 1) + 8 * ((lane >> 2) & 1) + 4 * ((lane >> 1) & 1) + 2 * (lane & 1)
-                   : 16 * ((lane >> 2) & 1) + 8 * ((lane >> 1) & 1) + 4 * (lane & 1);
+__device__ __forceinline__ int strided_rs_base(int lane) {
+    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + 2 * ((lane >> 2) & 1);
 }
-__device__ __forceinline__ void tri6(int t, int& r, int& s) {   // packed upper index t < 21 -> (r, s), r <= s
-    r = 0;
-    int rem = t;
-    while (rem >= 6 - r) { rem -= 6 - r; ++r; }
-    s = r + rem;
+// packed upper index t < 21 -> (r, s), r <= s, without a loop: r from a 3-bit-per-entry table
+__device__ __forceinline__ void tri6(int t, int& r, int& s) {
+    constexpr unsigned long long kRow = 0ull | (1ull << 18) | (1ull << 21) | (1ull << 24) | (1ull << 27) |
+                                        (1ull << 30) | (2ull << 33) | (2ull << 36) | (2ull << 39) | (2ull << 42) |
+                                        (3ull << 45) | (3ull << 48) | (3ull << 51) | (4ull << 54) | (4ull << 57) |
+                                        (5ull << 60);
+    r = (int)((kRow >> (3 * t)) & 7);
+    s = t - 6 * r + r * (r - 1) / 2 + r;   // t - (row start 6r - r(r-1)/2) + r
 }
 
 constexpr int kEdgeChunk = 96;    // corners of one edge staged in LDS at a time (k_edge)
 #ifndef MCC_EDGE_WAVES
 #define MCC_EDGE_WAVES 4            // k_edge waves per SIMD (register budget 128 VGPRs)
 #endif
+// 16 lanes per edge, 4 edges per one-wave workgroup, lanes strided: edge g = lane & 3 owns lanes
+// g, g + 4, ..., g + 60 (sub = lane >> 2), so the butterfly's two widest exchanges are permlane
+// swaps and the staged corners are read at consecutive LDS addresses.
 template <int MODEL, bool RATIONAL, bool PRISM, int L>
 __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) ? 3 : MCC_EDGE_WAVES) void k_edge(LinArgs a) {
+    static_assert(L == 16, "k_edge: 16 lanes per edge");
     if (a.state->done) return;
     constexpr int GPB = 64 / L;   // edges per workgroup (one wave)
-    const int tid = threadIdx.x, g = tid / L, sub = tid % L;
+    const int tid = threadIdx.x, g = tid % GPB, sub = tid / GPB;
     const int e = blockIdx.x * GPB + g;
     long long* stp = (a.stamps && (int)(blockIdx.x / 2) < a.n_photos)
                          ? a.stamps + kStampStride * (size_t)(blockIdx.x / 2) + 16 + 8 * (blockIdx.x & 1) : nullptr;
     SSTAMP(stp, 0, 0);
-    // LDS per wave: the staged corners, reused after the sweep for the chain (A', b', G, X), and the
-    // edge's pose / camera (8.6 KB: 4 waves per SIMD)
-    struct Chain { double A[36], B[6], G[72], X[72]; };
-    __shared__ __attribute__((aligned(16))) union { float C[GPB][5][kEdgeChunk]; Chain H[GPB]; } sU;
+    // LDS per wave: the staged corners [stream][corner][edge], reused after the sweep for the chain
+    // (A', b', the chain maps' nonzero blocks, X = A' G), and the edge's pose / camera (8.6 KB: 4
+    // waves per SIMD)
+    struct Chain {
+        double A[36], B[8];
+        double Gb[2][28];   // [photo | global] nonzero 3x3 blocks G11, G21, G22 (27 + pad)
+        double X[2][6][8];  // X_p = [A' Gp | b'], X_g = A' Gg (rows of 8: 16-B aligned)
+    };
+    __shared__ __attribute__((aligned(16))) union { float C[5][kEdgeChunk][GPB]; Chain H[GPB]; } sU;
     __shared__ double sP[GPB][30];
     __shared__ int sI[GPB][2];   // corner offset and count, re-read per chunk (nothing stays live through the sweep)
     auto& sC = sU.C;
-    if (e >= a.n_edges) return;   // whole groups: L divides the wave
+    if (e >= a.n_edges) return;   // the partner lanes of every exchange belong to the same edge
     const int4 info = a.edge_info[e];
     const int cam = info.x, off = info.z, n = info.w;
     if (sub == 0) {
         sI[g][0] = off;
         sI[g][1] = n;
     }
-    // the edge's corners (contiguous in all five streams) -> LDS, every load in flight at once;
-    // chain maps (consumed after the sweep) expanded into Gp, Gg (6 x 6)
+    // the edge's corners (contiguous in all five streams) -> LDS, every load in flight at once
     auto stage = [&](int eoff, int c0, int cn) {   // every load of the chunk issued before the first LDS store
         constexpr int PER = kEdgeChunk / L;
         float v[PER][5];
@@ -1715,7 +1709,7 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
             const int i = sb + L * u;
             if (i < cn) {
 #pragma unroll
-                for (int f = 0; f < 5; ++f) sC[g][f][i] = v[u][f];
+                for (int f = 0; f < 5; ++f) sC[f][i][g] = v[u][f];
             }
         }
     };
@@ -1764,8 +1758,8 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
 #pragma unroll
             for (int q = 0; q < 12; ++q) kd[q] = P[18 + q];
             const double fx = P[12], fy = P[13], cx = P[14], cy = P[15], sk = P[16], xi = P[17];
-            const double X = sC[g][0][i], Y = sC[g][1][i], Z = sC[g][2][i];
-            const float ou = sC[g][3][i], ov = sC[g][4][i];
+            const double X = sC[0][i][g], Y = sC[1][i][g], Z = sC[2][i][g];
+            const float ou = sC[3][i][g], ov = sC[4][i][g];
             double Yr[3], D[6];
             float u, v;
             if (MODEL == MCC_MODEL_OMNI)
@@ -1802,28 +1796,27 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
     // (not e, g, sub and their addresses) stays live through the sweep at 128 VGPRs
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    const int gq = tq / L, sq = tq % L;
+    const int gq = tq % GPB, sq = tq / GPB;
     const int eq = blockIdx.x * GPB + gq;
-    group_reduce_scatter<L>(acc, tq);
+    // the chain maps' nonzero blocks (echain: Gp11, Gp21, Gp22, Gg11, Gg21, Gg22), loaded before
+    // the butterfly so that it covers their latency
+    const double* ec = a.echain + 54 * (size_t)eq;
+    double gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gv[u] = sq + L * u < 54 ? ec[sq + L * u] : 0.0;
+    strided_reduce_scatter16(acc, tq);
     wave_sync_lds();   // the corners are consumed: the union's chain view from here on
     SSTAMP(stp, 3, 0);
     Chain& CH = sU.H[gq];
-    {   // chain maps: the nonzero 3 x 3 blocks -> Gp, Gg (6 x 6)
-        const double* ec = a.echain + 54 * (size_t)eq;
-        for (int t = sq; t < 72; t += L) {
-            const int w = t / 36, r = (t % 36) / 6, c = t % 6;
-            const double* gb = ec + 27 * w;
-            double v = 0.0;
-            if (r < 3 && c < 3) v = gb[r * 3 + c];
-            else if (r >= 3 && c < 3) v = gb[9 + (r - 3) * 3 + c];
-            else if (r >= 3) v = gb[18 + (r - 3) * 3 + c - 3];
-            CH.G[t] = v;
-        }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int t = sq + L * u;
+        if (t < 54) CH.Gb[t / 27][t % 27] = gv[u];
     }
     {
-        const int base = group_rs_base<L>(tq);
+        const int base = strided_rs_base(tq);
 #pragma unroll
-        for (int q = 0; q < 32 / L; ++q) {
+        for (int q = 0; q < 2; ++q) {
             const int idx = base + q;
             if (idx < 21) {
                 int r, s2;
@@ -1836,74 +1829,82 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
         }
     }
     wave_sync_lds();
-    // X = A' G (A' symmetric): lane (w, i) < 12 forms row i of X_w, its operands (A' row i, all of
-    // G_w) read at once (16-B LDS reads: one round trip)
+    // X_w = A' G_w with G_w = [[G11, 0], [G21, G22]] (A' symmetric): lane (w, i) < 12 forms row i,
+    // the zero block skipped (the same FMA sequence as the dense 6 x 6 product minus its exact-zero
+    // terms); X_p carries b' as a seventh column, so that G^T X_p also yields g = G^T b'
     if (sq < 12) {
         const int w = sq / 6, i = sq % 6;
-        double ar[6], gm[36], xr[6];
+        double ar[6], gm[28], xr[8];
         const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
-        const double2* G2 = reinterpret_cast<const double2*>(CH.G + 36 * w);
+        const double2* G2 = reinterpret_cast<const double2*>(CH.Gb[w]);
 #pragma unroll
         for (int q = 0; q < 3; ++q) { const double2 v = A2[q]; ar[2 * q] = v.x; ar[2 * q + 1] = v.y; }
 #pragma unroll
-        for (int q = 0; q < 18; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
+        for (int q = 0; q < 14; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
+        for (int j = 0; j < 3; ++j) {
             double s2 = 0.0;
 #pragma unroll
-            for (int k = 0; k < 6; ++k) s2 += ar[k] * gm[k * 6 + j];
-            xr[j] = s2;
-        }
-        double2* X2 = reinterpret_cast<double2*>(CH.X + 36 * w + 6 * i);
+            for (int k = 0; k < 3; ++k) s2 += ar[k] * gm[k * 3 + j];            // G11
 #pragma unroll
-        for (int q = 0; q < 3; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
+            for (int k = 0; k < 3; ++k) s2 += ar[3 + k] * gm[9 + k * 3 + j];   // G21
+            xr[j] = s2;
+            double s3 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s3 += ar[3 + k] * gm[18 + k * 3 + j];  // G22
+            xr[3 + j] = s3;
+        }
+        xr[6] = w == 0 ? CH.B[i] : 0.0;
+        xr[7] = 0.0;
+        double2* X2 = reinterpret_cast<double2*>(CH.X[w][i]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
     }
     wave_sync_lds();
-    // H = G^T X, g = G^T b':  eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Tasks:
-    // rows i of Hpp (Gp, Xp), Hgg (Gg, Xg), Hgp (Gg, Xp: rows global, columns photo), then gp, gg
-    double* out = a.eh + 90 * (size_t)eq;
-    for (int task = sq; task < 20; task += L) {
-        if (task < 18) {
-            const int blk = task / 6, i = task % 6;
-            const double* Gl = CH.G + (blk == 0 ? 0 : 36);
-            const double2* X2 = reinterpret_cast<const double2*>(CH.X + (blk == 1 ? 36 : 0));
-            double gc[6], xm[36];
+    // H = G_l^T X_r: eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Lane (T, i) < 9
+    // forms rows i and i + 3 of (T = 0) Gp^T [Xp | b'] -> Hpp, gp; (1) Gg^T [Xp | b'] -> Hgp, gg;
+    // (2) Gg^T Xg -> Hgg.  Row i < 3 takes G11 and G21, row i + 3 only G22 (zero block skipped).
+    if (sq < 9) {
+        const int T = sq / 3, i = sq % 3;
+        const double* Gl = CH.Gb[T == 0 ? 0 : 1];
+        const double2* X2 = reinterpret_cast<const double2*>(CH.X[T == 2 ? 1 : 0][0]);
+        double c11[3], c21[3], c22[3];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) gc[k] = Gl[k * 6 + i];   // column i of G
+        for (int k = 0; k < 3; ++k) {
+            c11[k] = Gl[k * 3 + i];
+            c21[k] = Gl[9 + k * 3 + i];
+            c22[k] = Gl[18 + k * 3 + i];
+        }
+        double h[7], h2[7];
 #pragma unroll
-            for (int q = 0; q < 18; ++q) { const double2 v = X2[q]; xm[2 * q] = v.x; xm[2 * q + 1] = v.y; }
-            double h[6];
+        for (int j = 0; j < 7; ++j) { h[j] = 0.0; h2[j] = 0.0; }
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double s2 = 0.0;
+        for (int k = 0; k < 6; ++k) {
+            double xk[8];
 #pragma unroll
-                for (int k = 0; k < 6; ++k) s2 += gc[k] * xm[k * 6 + j];
-                h[j] = s2;
+            for (int q = 0; q < 4; ++q) { const double2 v = X2[4 * k + q]; xk[2 * q] = v.x; xk[2 * q + 1] = v.y; }
+            const double c = k < 3 ? c11[k] : c21[k - 3];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) h[j] += c * xk[j];
+            if (k >= 3) {
+#pragma unroll
+                for (int j = 0; j < 7; ++j) h2[j] += c22[k - 3] * xk[j];
             }
-            if (blk < 2) {   // upper row i: packed at 21 blk + 6 i - i (i - 1) / 2, columns j >= i
-                double* o = out + 21 * blk + 6 * i - i * (i - 1) / 2 - i;
+        }
+        double* out = a.eh + 90 * (size_t)eq;
+        const bool tri = T != 1;
+        const int i2 = i + 3;
+        const int blk = T == 2 ? 21 : 0;
+        double* o1 = tri ? out + blk + 6 * i - i * (i - 1) / 2 - i : out + 42 + 6 * i;
+        double* o2 = tri ? out + blk + 6 * i2 - i2 * (i2 - 1) / 2 - i2 : out + 42 + 6 * i2;
 #pragma unroll
-                for (int j = 0; j < 6; ++j)
-                    if (j >= i) o[j] = h[j];
-            } else {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) out[42 + 6 * i + j] = h[j];
-            }
-        } else {
-            const int w = task - 18;
-            const double2* G2 = reinterpret_cast<const double2*>(CH.G + 36 * w);
-            double gm[36], b[6];
-#pragma unroll
-            for (int q = 0; q < 18; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
-#pragma unroll
-            for (int k = 0; k < 6; ++k) b[k] = CH.B[k];
-#pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                double s2 = 0.0;
-#pragma unroll
-                for (int k = 0; k < 6; ++k) s2 += gm[k * 6 + j] * b[k];
-                out[78 + 6 * w + j] = s2;
-            }
+        for (int j = 0; j < 6; ++j) {
+            if (!tri || j >= i) o1[j] = h[j];
+            if (!tri || j >= i2) o2[j] = h2[j];
+        }
+        if (T < 2) {
+            out[78 + 6 * T + i] = h[6];
+            out[78 + 6 * T + i2] = h2[6];
         }
     }
 #ifdef MCC_DIAG
