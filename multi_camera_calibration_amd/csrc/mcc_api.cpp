@@ -160,7 +160,7 @@ struct mcc_problem {
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
-    DevBuf<int> pgrp_ptr, gpair_ptr, gcon_ptr;
+    DevBuf<int> pgrp_ptr, pgrp_edge, gpair_ptr, gcon_ptr;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
     DevBuf<State> state;
@@ -240,7 +240,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
     la.Y = p->Y.p; la.zp = p->zp.p;
-    la.pgrp_ptr = p->pgrp_ptr.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
+    la.pgrp_ptr = p->pgrp_ptr.p; la.pgrp_edge = p->pgrp_edge.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
     la.gcon_ptr = p->gcon_ptr.p; la.gcon = p->gcon.p; la.pairprod = p->pairprod.p;
     la.n_pgroups = p->n_pgroups; la.max_gpairs = p->max_gpairs; la.max_gcon = p->max_gcon; la.max_gedges = p->max_gedges;
     la.gp_tot = p->gp_tot.p;
@@ -676,6 +676,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->ds_rt.upload(ds_rt, 6));
     HIPC(p->alpha.upload(alpha.data(), alpha.size()));
     HIPC(p->pgrp_ptr.upload(pgrp_ptr.data(), pgrp_ptr.size()));
+    {
+        std::vector<int> pgrp_edge(pgrp_ptr.size());
+        for (size_t g = 0; g < pgrp_ptr.size(); ++g) pgrp_edge[g] = photo_ptr[pgrp_ptr[g]];
+        HIPC(p->pgrp_edge.upload(pgrp_edge.data(), pgrp_edge.size()));
+    }
     HIPC(p->gpair_ptr.upload(gpair_ptr.data(), gpair_ptr.size()));
     HIPC(p->gpairs.upload(gpairs.data(), gpairs.size()));
     HIPC(p->gcon_ptr.upload(gcon_ptr.data(), gcon_ptr.size()));
@@ -753,7 +758,7 @@ void mcc_destroy(mcc_problem* p) {
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->gpairs.release();
-    p->pgrp_ptr.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
+    p->pgrp_ptr.release(); p->pgrp_edge.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused

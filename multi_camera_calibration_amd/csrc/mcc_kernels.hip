@@ -1459,7 +1459,7 @@ __device__ __forceinline__ void camera_pose_lds(const double* cam6, int cam, dou
 template <int MODEL, bool BACK>
 __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     const State* st = a.state;
-    if (st->done) return;
+    const int done = st->done;   // tested after the first round trip's loads are issued
     const int tid = threadIdx.x, grp = tid / kPrepGroup, l = tid % kPrepGroup;
     const int photo = blockIdx.x * (64 / kPrepGroup) + grp;
     long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)blockIdx.x + 8 : nullptr;   // MCC_DIAG
@@ -1483,6 +1483,7 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     for (int q = tid; q < a.global_dim; q += 64) s_dg[q] = a.dg[q];
     if (BACK && tid < 6) s_ds[tid] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[tid] : a.ds_rt[tid];
     wave_sync_lds();
+    if (done) return;
     float* xg = a.x + a.global_dim + 6 * (size_t)photo;
     // the camera of the lane's first edge: Rodrigues + Jl, independent of the photo update
     int4 info0 = make_int4(0, 0, 0, 0);
@@ -1921,16 +1922,25 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
 // the Schur pair products ([self] Hgg_a - Y'_a Hgp_b^T = U_a U_b^T, [self] (gg_a - U_a v),
 // [self] gg_a), written once per group at the block's slot (k_schur sums the slots).  Summing in
 // the group first cuts the slots (and k_schur's reads) to ~40% at 8 photos per group on config3.
+#ifndef MCC_PHOTO_RPT
+#define MCC_PHOTO_RPT 1   // rows of a camera-pair block per k_photo pair task (2, 3: fewer waves, slower)
+#endif
+#ifdef MCC_PHOTO_OCC
+__global__ __launch_bounds__(256, MCC_PHOTO_OCC) void k_photo(LinArgs a) {
+#else
 __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
+#endif
     State* st = a.state;
-    if (st->done) return;
     const int grp = blockIdx.x, tid = threadIdx.x;
     long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)grp : nullptr;   // MCC_DIAG: slots 0..7
     SSTAMP(stp, 0, 0);
+    // one round trip: the state and every per-group range (the stop test after the loads are issued)
+    const int done = st->done;
     const int p0 = a.pgrp_ptr[grp], np = a.pgrp_ptr[grp + 1] - p0;
-    const int ge0 = a.photo_ptr[p0], gne = a.photo_ptr[p0 + np] - ge0;   // the group's edges are contiguous
+    const int ge0 = a.pgrp_edge[grp], gne = a.pgrp_edge[grp + 1] - ge0;   // the group's edges are contiguous
     const int q0 = a.gpair_ptr[grp], nq = a.gpair_ptr[grp + 1] - q0;
     const int c0 = a.gcon_ptr[grp], nc = a.gcon_ptr[grp + 1] - c0;
+    if (done) return;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int ES = 64;                      // per edge: Hgg upper [0, 21), pad, U [22, 58), gg [58, 64)
     double* sE = smem;                          // [gne][ES]
@@ -2098,63 +2108,89 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
     }
     __syncthreads();
     SSTAMP(stp, 4, 0);
-    // task (block pair k, row i, part h of H): the group's contributions c = h, h + H, ... (photo,
-    // then edge pair order) summed by each part, the H parts (consecutive lanes) combined by a
-    // fixed xor butterfly.  H > 1 only when the group has few block pairs (a one-block rig:
-    // DoubleSide, every edge pair of the group lands in one slot) so the threads stay busy.
+    // task (block pair k, rows i0 .. i0 + RPT - 1, part h of H): the group's contributions c = h, h + H,
+    // ... (photo, then edge pair order) summed by each part, the H parts (consecutive lanes)
+    // combined by a fixed xor butterfly.  RPT = 2 rows per task: U_b is read once for both (three
+    // tasks per block pair; three rows would spill at 3 waves per SIMD), and each entry keeps its
+    // summation order.  H > 1 only when the group has few block
+    // pairs (a one-block rig: DoubleSide, every edge pair of the group lands in one slot) so the
+    // threads stay busy.
+    constexpr int RPT = MCC_PHOTO_RPT, NT = 6 / RPT;
     int H = 1;
-    while (H < 32 && 6 * nq * 2 * H <= 256) H *= 2;
-    for (int t = tid; t < 6 * nq * H; t += 256) {
-        const int h = t % H, k = t / H / 6, i = (t / H) % 6;
+    while (H < 32 && NT * nq * 2 * H <= 256) H *= 2;
+    for (int t = tid; t < NT * nq * H; t += 256) {
+        const int h = t % H, k = t / H / NT, i0 = RPT * ((t / H) % NT);
         const int4 pq = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}
         const bool diag = (pq.z & 2) != 0;
-        double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, racc = 0.0, jacc = 0.0;
+        double acc[RPT][6], racc[RPT], jacc[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            racc[r] = 0.0;
+            jacc[r] = 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) acc[r][j] = 0.0;
+        }
+#pragma unroll 1
         for (int c = pq.x + h; c < pq.x + pq.y; c += H) {
             const unsigned w = scn[c];
             const int ea = w & 255, eb = (w >> 8) & 255, q = w >> 17;
             const bool self = (w >> 16) & 1;
-            const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * ea + 22 + 6 * i);
+            const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * ea + 22 + 6 * i0);
             const double2* B2 = reinterpret_cast<const double2*>(sE + ES * eb + 22);
-            double y[6], Hb[36];
+            double y[6 * RPT];
 #pragma unroll
-            for (int qq = 0; qq < 3; ++qq) { const double2 v = Y2[qq]; y[2 * qq] = v.x; y[2 * qq + 1] = v.y; }
-#pragma unroll
-            for (int qq = 0; qq < 18; ++qq) { const double2 v = B2[qq]; Hb[2 * qq] = v.x; Hb[2 * qq + 1] = v.y; }
+            for (int qq = 0; qq < 3 * RPT; ++qq) { const double2 v = Y2[qq]; y[2 * qq] = v.x; y[2 * qq + 1] = v.y; }
             const double* Hgg = sE + ES * ea;
 #pragma unroll
             for (int j = 0; j < 6; ++j) {
-                double d = 0.0;
+                double hb[6];
 #pragma unroll
-                for (int kk = 0; kk < 6; ++kk) d += y[kk] * Hb[j * 6 + kk];
-                double h = 0.0;
-                if (self) {
-                    const int r = i < j ? i : j, cc = i < j ? j : i;
-                    h = Hgg[r * 6 - r * (r - 1) / 2 + (cc - r)];
+                for (int qq = 0; qq < 3; ++qq) { const double2 v = B2[3 * j + qq]; hb[2 * qq] = v.x; hb[2 * qq + 1] = v.y; }
+#pragma unroll
+                for (int r = 0; r < RPT; ++r) {
+                    const int i = i0 + r;
+                    double d = 0.0;
+#pragma unroll
+                    for (int kk = 0; kk < 6; ++kk) d += y[6 * r + kk] * hb[kk];
+                    double hv = 0.0;
+                    if (self) {
+                        const int rr = i < j ? i : j, cc = i < j ? j : i;
+                        hv = Hgg[rr * 6 - rr * (rr - 1) / 2 + (cc - rr)];
+                    }
+                    acc[r][j] += self ? hv - d : -d;
                 }
-                acc[j] += self ? h - d : -d;
             }
             if (diag && self) {
-                double d = 0.0;
 #pragma unroll
-                for (int kk = 0; kk < 6; ++kk) d += y[kk] * sv[6 * q + kk];
-                const double gg = sE[ES * ea + 58 + i];
-                racc += gg - d;
-                jacc += gg;
+                for (int r = 0; r < RPT; ++r) {
+                    double d = 0.0;
+#pragma unroll
+                    for (int kk = 0; kk < 6; ++kk) d += y[6 * r + kk] * sv[6 * q + kk];
+                    const double gg = sE[ES * ea + 58 + i0 + r];
+                    racc[r] += gg - d;
+                    jacc[r] += gg;
+                }
             }
         }
         for (int o = 1; o < H; o <<= 1) {   // the H parts are lanes t - h .. t - h + H - 1 (H | 64)
 #pragma unroll
-            for (int j = 0; j < 6; ++j) acc[j] += __shfl_xor(acc[j], o);
-            racc += __shfl_xor(racc, o);
-            jacc += __shfl_xor(jacc, o);
+            for (int r = 0; r < RPT; ++r) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) acc[r][j] += __shfl_xor(acc[r][j], o);
+                racc[r] += __shfl_xor(racc[r], o);
+                jacc[r] += __shfl_xor(jacc[r], o);
+            }
         }
         if (h == 0) {
             double* out = a.pairprod + (size_t)pq.w;
 #pragma unroll
-            for (int j = 0; j < 6; ++j) out[i * 6 + j] = acc[j];
-            if (diag) {
-                out[36 + i] = racc;
-                out[42 + i] = jacc;
+            for (int r = 0; r < RPT; ++r) {
+#pragma unroll
+                for (int j = 0; j < 6; ++j) out[(i0 + r) * 6 + j] = acc[r][j];
+                if (diag) {
+                    out[36 + i0 + r] = racc[r];
+                    out[42 + i0 + r] = jacc[r];
+                }
             }
         }
     }
