@@ -161,6 +161,7 @@ struct mcc_problem {
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
     DevBuf<int> pgrp_ptr, pgrp_edge, gpair_ptr, gcon_ptr;
+    DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
     DevBuf<State> state;
@@ -240,7 +241,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
     la.Y = p->Y.p; la.zp = p->zp.p;
-    la.pgrp_ptr = p->pgrp_ptr.p; la.pgrp_edge = p->pgrp_edge.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
+    la.pgrp_ptr = p->pgrp_ptr.p; la.pgrp_edge = p->pgrp_edge.p; la.edge_lphoto = p->edge_lphoto.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
     la.gcon_ptr = p->gcon_ptr.p; la.gcon = p->gcon.p; la.pairprod = p->pairprod.p;
     la.n_pgroups = p->n_pgroups; la.max_gpairs = p->max_gpairs; la.max_gcon = p->max_gcon; la.max_gedges = p->max_gedges;
     la.gp_tot = p->gp_tot.p;
@@ -680,6 +681,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         std::vector<int> pgrp_edge(pgrp_ptr.size());
         for (size_t g = 0; g < pgrp_ptr.size(); ++g) pgrp_edge[g] = photo_ptr[pgrp_ptr[g]];
         HIPC(p->pgrp_edge.upload(pgrp_edge.data(), pgrp_edge.size()));
+        std::vector<unsigned char> lph(std::max(E, 1), 0);
+        for (size_t g = 0; g + 1 < pgrp_ptr.size(); ++g)
+            for (int v = pgrp_ptr[g]; v < pgrp_ptr[g + 1]; ++v)
+                for (int e = photo_ptr[v]; e < photo_ptr[v + 1]; ++e) lph[e] = (unsigned char)(v - pgrp_ptr[g]);
+        HIPC(p->edge_lphoto.upload(lph.data(), lph.size()));
     }
     HIPC(p->gpair_ptr.upload(gpair_ptr.data(), gpair_ptr.size()));
     HIPC(p->gpairs.upload(gpairs.data(), gpairs.size()));
@@ -758,7 +764,7 @@ void mcc_destroy(mcc_problem* p) {
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->gpairs.release();
-    p->pgrp_ptr.release(); p->pgrp_edge.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
+    p->pgrp_ptr.release(); p->pgrp_edge.release(); p->edge_lphoto.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused

@@ -68,6 +68,7 @@ struct LinArgs {
     // block and writes them at that block's slot (block-major over the groups; k_schur sums them)
     const int* pgrp_ptr;     // [n_pgroups + 1] first photo of each group
     const int* pgrp_edge;    // [n_pgroups + 1] first edge of each group (photo_ptr[pgrp_ptr[g]])
+    const unsigned char* edge_lphoto;   // [E] an edge's photo within its group (0 .. kPhotoGroup - 1)
     const int* gpair_ptr;    // [n_pgroups + 1] ranges of gpairs
     const int4* gpairs;      // {first contribution (group-relative), count, diagonal block << 1, slot offset}
     const int* gcon_ptr;     // [n_pgroups + 1] ranges of gcon

@@ -1978,6 +1978,7 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) sv0[u] = (sl && u < pne) ? src[90 * (pe0 + u) + col] : 0.0;
         const int gbv = tid < gne ? a.gblock[ge0 + tid] : -1;
+        const int lpv = tid < gne ? a.edge_lphoto[ge0 + tid] : 0;
         const int4 pqv = tid < nq ? a.gpairs[q0 + tid] : make_int4(0, 0, 0, 0);
         const unsigned cnv = tid < nc ? a.gcon[c0 + tid] : 0u;
 #pragma unroll
@@ -1999,10 +2000,8 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
         }
         if (tid < gne) sgb[tid] = gbv;
         for (int t = tid + 256; t < gne; t += 256) sgb[t] = a.gblock[ge0 + t];
-        for (int q = 0; q < np; ++q) {   // edge -> group-local photo
-            const int b = a.photo_ptr[p0 + q] - ge0, e = a.photo_ptr[p0 + q + 1] - ge0;
-            for (int t = b + tid; t < e; t += 256) seq[t] = q;
-        }
+        if (tid < gne) seq[tid] = lpv;   // edge -> group-local photo (host-built, first round trip)
+        for (int t = tid + 256; t < gne; t += 256) seq[t] = a.edge_lphoto[ge0 + t];
         if (tid < nq) spq[tid] = pqv;
         for (int t = tid + 256; t < nq; t += 256) spq[t] = a.gpairs[q0 + t];
         if (tid < nc) scn[tid] = cnv;
