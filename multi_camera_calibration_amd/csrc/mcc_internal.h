@@ -102,6 +102,7 @@ struct LinArgs {
     double* eh;              // [90E] Hpp upper (21), Hgg upper (21), Hgp (36), gp (6), gg (6) (k_edge -> k_photo)
 };
 
+constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
 constexpr int kPhotoGroup = 8;        // photos per k_photo workgroup, at most
 constexpr int kPhotoGroupEdges = 64;  // edges per k_photo workgroup, at most
 // k_photo's LDS (doubles, then ints): per edge [Hgg upper 21 | pad | U 36 | gg 6] (64), per photo the

@@ -1602,12 +1602,12 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     SSTAMP(stp, 3, 0);
 }
 
-// Reduce-scatter of 32 per-lane values over the 16 lanes {g, g + 4, ..., g + 60} of one edge
-// (k_edge's strided lane map, g = lane & 3): xor 32 and 16 as whole half-wave / row swaps
+// Reduce-scatter of 32 per-lane values over the L lanes {g, g + 64/L, ...} of one edge (k_edge's
+// strided lane map, g = lane % (64/L)): xor 32 and 16 as whole half-wave / row swaps
 // (v_permlane32_swap, v_permlane16_swap: two instructions and an add per value pair instead of
 // selects around DPP), xor 8 and 4 by DPP inside a row.  In the edge's own numbering
-// (sub = lane >> 2) this is the fixed tree sub ^ 8, ^ 4, ^ 2, ^ 1.  Afterwards the lane holds the
-// edge's sums of value indices strided_rs_base(lane) + {0, 1}.
+// (sub = lane / (64/L)) this is the fixed tree sub ^ (L/2), ..., ^ 1.  Afterwards the lane holds
+// the edge's sums of value indices strided_rs_base<L>(lane) + {0 .. 32/L - 1}.
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64u(double v) {   // no 'old' operand to initialise
     const unsigned long long b = __double_as_longlong(v);
@@ -1615,12 +1615,14 @@ __device__ __forceinline__ double dpp_f64u(double v) {   // no 'old' operand to 
     const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, false);
     return ull_f64((unsigned)lo, (unsigned)hi);
 }
-__device__ __forceinline__ void strided_reduce_scatter16(double* v, int lane) {
+template <int L>
+__device__ __forceinline__ void strided_reduce_scatter(double* v, int lane) {
+    static_assert(L == 16 || L == 8, "lanes per edge");
 #pragma unroll
-    for (int j = 0; j < 16; ++j) { double p = v[j], q = v[j + 16]; pl32_swap(p, q); v[j] = p + q; }   // sub ^ 8
+    for (int j = 0; j < 16; ++j) { double p = v[j], q = v[j + 16]; pl32_swap(p, q); v[j] = p + q; }   // lane ^ 32
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { double p = v[j], q = v[j + 8]; pl16_swap(p, q); v[j] = p + q; }     // sub ^ 4
-    {   // sub ^ 2 = lane ^ 8: rotate a row by 8
+    for (int j = 0; j < 8; ++j) { double p = v[j], q = v[j + 8]; pl16_swap(p, q); v[j] = p + q; }     // lane ^ 16
+    {   // lane ^ 8: rotate a row by 8
         const bool hi = (lane & 8) != 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1628,7 +1630,7 @@ __device__ __forceinline__ void strided_reduce_scatter16(double* v, int lane) {
             v[j] = keep + dpp_f64u<kDppRor8>(send);
         }
     }
-    {   // sub ^ 1 = lane ^ 4: i - 4 for the upper, i + 4 = i - 12 for the lower
+    if (L == 16) {   // lane ^ 4: i - 4 for the upper, i + 4 = i - 12 for the lower
         const bool hi = (lane & 4) != 0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1638,8 +1640,9 @@ __device__ __forceinline__ void strided_reduce_scatter16(double* v, int lane) {
         }
     }
 }
+template <int L>
 __device__ __forceinline__ int strided_rs_base(int lane) {
-    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + 2 * ((lane >> 2) & 1);
+    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + (L == 16 ? 2 * ((lane >> 2) & 1) : 0);
 }
 // packed upper index t < 21 -> (r, s), r <= s, without a loop: r from a 3-bit-per-entry table
 __device__ __forceinline__ void tri6(int t, int& r, int& s) {
@@ -1651,18 +1654,110 @@ __device__ __forceinline__ void tri6(int t, int& r, int& s) {
     s = t - 6 * r + r * (r - 1) / 2 + r;   // t - (row start 6r - r(r-1)/2) + r
 }
 
+// One edge's chain H = G^T A' G, g = G^T b' from its LDS record (A', b', the chain maps' nonzero
+// blocks), by the edge's 16 lanes sq = 0 .. 15 (every lane of the wave calls it: wave-level syncs).
+struct EdgeChain {
+    double A[36], B[8];
+    double Gb[2][28];   // [photo | global] nonzero 3x3 blocks G11, G21, G22 (27 + pad)
+    double X[2][6][8];  // X_p = [A' Gp | b'], X_g = A' Gg (rows of 8: 16-B aligned)
+};
+__device__ __forceinline__ void edge_chain_xh(EdgeChain& CH, int sq, int eq, bool valid, const LinArgs& a) {
+    // X_w = A' G_w with G_w = [[G11, 0], [G21, G22]] (A' symmetric): lane (w, i) < 12 forms row i,
+    // the zero block skipped (the same FMA sequence as the dense 6 x 6 product minus its exact-zero
+    // terms); X_p carries b' as a seventh column, so that G^T X_p also yields g = G^T b'
+    if (sq < 12) {
+        const int w = sq / 6, i = sq % 6;
+        double ar[6], gm[28], xr[8];
+        const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
+        const double2* G2 = reinterpret_cast<const double2*>(CH.Gb[w]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) { const double2 v = A2[q]; ar[2 * q] = v.x; ar[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < 14; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s2 += ar[k] * gm[k * 3 + j];            // G11
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s2 += ar[3 + k] * gm[9 + k * 3 + j];   // G21
+            xr[j] = s2;
+            double s3 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s3 += ar[3 + k] * gm[18 + k * 3 + j];  // G22
+            xr[3 + j] = s3;
+        }
+        xr[6] = w == 0 ? CH.B[i] : 0.0;
+        xr[7] = 0.0;
+        double2* X2 = reinterpret_cast<double2*>(CH.X[w][i]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
+    }
+    wave_sync_lds();
+    // H = G_l^T X_r: eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Lane (T, i) < 9
+    // forms rows i and i + 3 of (T = 0) Gp^T [Xp | b'] -> Hpp, gp; (1) Gg^T [Xp | b'] -> Hgp, gg;
+    // (2) Gg^T Xg -> Hgg.  Row i < 3 takes G11 and G21, row i + 3 only G22 (zero block skipped).
+    if (sq < 9 && valid) {
+        const int T = sq / 3, i = sq % 3;
+        const double* Gl = CH.Gb[T == 0 ? 0 : 1];
+        const double2* X2 = reinterpret_cast<const double2*>(CH.X[T == 2 ? 1 : 0][0]);
+        double c11[3], c21[3], c22[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            c11[k] = Gl[k * 3 + i];
+            c21[k] = Gl[9 + k * 3 + i];
+            c22[k] = Gl[18 + k * 3 + i];
+        }
+        double h[7], h2[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) { h[j] = 0.0; h2[j] = 0.0; }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            double xk[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { const double2 v = X2[4 * k + q]; xk[2 * q] = v.x; xk[2 * q + 1] = v.y; }
+            const double c = k < 3 ? c11[k] : c21[k - 3];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) h[j] += c * xk[j];
+            if (k >= 3) {
+#pragma unroll
+                for (int j = 0; j < 7; ++j) h2[j] += c22[k - 3] * xk[j];
+            }
+        }
+        double* out = a.eh + 90 * (size_t)eq;
+        const bool tri = T != 1;
+        const int i2 = i + 3;
+        const int blk = T == 2 ? 21 : 0;
+        double* o1 = tri ? out + blk + 6 * i - i * (i - 1) / 2 - i : out + 42 + 6 * i;
+        double* o2 = tri ? out + blk + 6 * i2 - i2 * (i2 - 1) / 2 - i2 : out + 42 + 6 * i2;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            if (!tri || j >= i) o1[j] = h[j];
+            if (!tri || j >= i2) o2[j] = h2[j];
+        }
+        if (T < 2) {
+            out[78 + 6 * T + i] = h[6];
+            out[78 + 6 * T + i2] = h2[6];
+        }
+    }
+}
+
 constexpr int kEdgeChunk = 96;    // corners of one edge staged in LDS at a time (k_edge)
 #ifndef MCC_EDGE_WAVES
 #define MCC_EDGE_WAVES 4            // k_edge waves per SIMD (register budget 128 VGPRs)
 #endif
-// 16 lanes per edge, 4 edges per one-wave workgroup, lanes strided: edge g = lane & 3 owns lanes
-// g, g + 4, ..., g + 60 (sub = lane >> 2), so the butterfly's two widest exchanges are permlane
-// swaps and the staged corners are read at consecutive LDS addresses.
+// L lanes per edge (16 or 8), 64 / L edges per one-wave workgroup, lanes strided: edge
+// g = lane % (64/L) owns lanes g, g + 64/L, ... (sub = lane / (64/L)), so the butterfly's widest
+// exchanges are permlane swaps and the staged corners are read at consecutive LDS addresses.
+// L = 8 sweeps an 88-corner edge in 11 full rounds (16 lanes: 5.5), halves the butterfly per
+// edge, and stages corners in 48-corner chunks; the chain then runs in passes of 4 edges with 16
+// lanes each (edge_chain_xh) so that its LDS fits in the corner area.
 template <int MODEL, bool RATIONAL, bool PRISM, int L>
 __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) ? 3 : MCC_EDGE_WAVES) void k_edge(LinArgs a) {
-    static_assert(L == 16, "k_edge: 16 lanes per edge");
+    static_assert(L == 16 || L == 8, "k_edge: 16 or 8 lanes per edge");
     if (a.state->done) return;
     constexpr int GPB = 64 / L;   // edges per workgroup (one wave)
+    constexpr int CHK = kEdgeChunk * L / 16;   // corners per staged chunk
     const int tid = threadIdx.x, g = tid % GPB, sub = tid / GPB;
     const int e = blockIdx.x * GPB + g;
     long long* stp = (a.stamps && (int)(blockIdx.x / 2) < a.n_photos)
@@ -1671,17 +1766,14 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
     // LDS per wave: the staged corners [stream][corner][edge], reused after the sweep for the chain
     // (A', b', the chain maps' nonzero blocks, X = A' G), and the edge's pose / camera (8.6 KB: 4
     // waves per SIMD)
-    struct Chain {
-        double A[36], B[8];
-        double Gb[2][28];   // [photo | global] nonzero 3x3 blocks G11, G21, G22 (27 + pad)
-        double X[2][6][8];  // X_p = [A' Gp | b'], X_g = A' Gg (rows of 8: 16-B aligned)
-    };
-    __shared__ __attribute__((aligned(16))) union { float C[5][kEdgeChunk][GPB]; Chain H[GPB]; } sU;
+    __shared__ __attribute__((aligned(16))) union { float C[5][CHK][GPB]; EdgeChain H[4]; } sU;
     __shared__ double sP[GPB][30];
     __shared__ int sI[GPB][2];   // corner offset and count, re-read per chunk (nothing stays live through the sweep)
     auto& sC = sU.C;
-    if (e >= a.n_edges) return;   // the partner lanes of every exchange belong to the same edge
-    const int4 info = a.edge_info[e];
+    // a workgroup's edges past the last are swept as empty (no early exit: the chain passes map
+    // lanes to edges differently from the sweep when L = 8)
+    const bool ev = e < a.n_edges;
+    const int4 info = ev ? a.edge_info[e] : make_int4(0, 0, 0, 0);
     const int cam = info.x, off = info.z, n = info.w;
     if (sub == 0) {
         sI[g][0] = off;
@@ -1689,7 +1781,7 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
     }
     // the edge's corners (contiguous in all five streams) -> LDS, every load in flight at once
     auto stage = [&](int eoff, int c0, int cn) {   // every load of the chunk issued before the first LDS store
-        constexpr int PER = kEdgeChunk / L;
+        constexpr int PER = CHK / L;
         float v[PER][5];
         int sb = sub;   // opaque: the lane's chunk offsets are recomputed per chunk, not kept live (spilled)
         asm volatile("" : "+v"(sb));
@@ -1714,14 +1806,14 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
             }
         }
     };
-    stage(off, 0, min(n, kEdgeChunk));
+    stage(off, 0, min(n, CHK));
     SSTAMP(stp, 1, 0);
     // the edge's pose and camera (R, T, fx, fy, cx, cy, skew, xi, k[12]) in LDS, re-read by every
     // corner (an opaque offset keeps the compiler from hoisting them into ~50 more VGPRs, which
     // would halve the waves per SIMD)
     {
         double* P = sP[g];
-        const double* er = a.erec + 12 * (size_t)e;
+        const double* er = a.erec + 12 * (size_t)(ev ? e : 0);
         const float* Kc = a.K + 9 * cam;
         const int nd = a.nd;
         for (int t = sub; t < 30; t += L) {
@@ -1737,10 +1829,10 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
 #pragma unroll
     for (int q = 0; q < 32; ++q) acc[q] = 0.0;
     wave_sync_lds();
-    for (int c0 = 0;; c0 += kEdgeChunk) {
+    for (int c0 = 0;; c0 += CHK) {
         const int nn = sI[g][1];
         if (c0 >= nn) break;
-        const int cn = min(nn - c0, kEdgeChunk);
+        const int cn = min(nn - c0, CHK);
         if (c0 > 0) {
             wave_sync_lds();   // the previous chunk is consumed
             stage(sI[g][0], c0, cn);
@@ -1797,116 +1889,49 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
     // (not e, g, sub and their addresses) stays live through the sweep at 128 VGPRs
     int tq = tid;
     asm volatile("" : "+v"(tq));
-    const int gq = tq % GPB, sq = tq / GPB;
-    const int eq = blockIdx.x * GPB + gq;
-    // the chain maps' nonzero blocks (echain: Gp11, Gp21, Gp22, Gg11, Gg21, Gg22), loaded before
-    // the butterfly so that it covers their latency
-    const double* ec = a.echain + 54 * (size_t)eq;
+    // the chain in passes of 4 edges, 16 lanes each: pass p takes edges 4p .. 4p + 3 of the
+    // workgroup, edge slot gq = tq & 3 with chain lane sq = tq >> 2 (for L = 16 the sweep's own map)
+    const int gq = tq & 3, sq = tq >> 2;
+    // the chain maps' nonzero blocks (echain: Gp11, Gp21, Gp22, Gg11, Gg21, Gg22) of the first
+    // pass, loaded before the butterfly so that it covers their latency
     double gv[4];
+    auto load_g = [&](int eq) {
+        const double* ec = a.echain + 54 * (size_t)(eq < a.n_edges ? eq : 0);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) gv[u] = sq + L * u < 54 ? ec[sq + L * u] : 0.0;
-    strided_reduce_scatter16(acc, tq);
-    wave_sync_lds();   // the corners are consumed: the union's chain view from here on
+        for (int u = 0; u < 4; ++u) gv[u] = sq + 16 * u < 54 ? ec[sq + 16 * u] : 0.0;
+    };
+    load_g(blockIdx.x * GPB + gq);
+    strided_reduce_scatter<L>(acc, tq);
     SSTAMP(stp, 3, 0);
-    Chain& CH = sU.H[gq];
+    const int gs = tq % GPB, base = strided_rs_base<L>(tq);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int t = sq + L * u;
-        if (t < 54) CH.Gb[t / 27][t % 27] = gv[u];
-    }
-    {
-        const int base = strided_rs_base(tq);
+    for (int pass = 0; pass < GPB / 4; ++pass) {
+        const int eq = blockIdx.x * GPB + 4 * pass + gq;
+        if (pass > 0) load_g(eq);
+        wave_sync_lds();   // the corners (pass 0) / the previous pass's records are consumed
+        EdgeChain& CH = sU.H[gq];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int idx = base + q;
-            if (idx < 21) {
-                int r, s2;
-                tri6(idx, r, s2);
-                CH.A[r * 6 + s2] = acc[q];
-                CH.A[s2 * 6 + r] = acc[q];
-            } else if (idx < 27) {
-                CH.B[idx - 21] = acc[q];
+        for (int u = 0; u < 4; ++u) {
+            const int t = sq + 16 * u;
+            if (t < 54) CH.Gb[t / 27][t % 27] = gv[u];
+        }
+        if (gs / 4 == pass) {   // this lane's reduced sums belong to an edge of the pass
+            EdgeChain& CW = sU.H[gs % 4];
+#pragma unroll
+            for (int q = 0; q < 32 / L; ++q) {
+                const int idx = base + q;
+                if (idx < 21) {
+                    int r, s2;
+                    tri6(idx, r, s2);
+                    CW.A[r * 6 + s2] = acc[q];
+                    CW.A[s2 * 6 + r] = acc[q];
+                } else if (idx < 27) {
+                    CW.B[idx - 21] = acc[q];
+                }
             }
         }
-    }
-    wave_sync_lds();
-    // X_w = A' G_w with G_w = [[G11, 0], [G21, G22]] (A' symmetric): lane (w, i) < 12 forms row i,
-    // the zero block skipped (the same FMA sequence as the dense 6 x 6 product minus its exact-zero
-    // terms); X_p carries b' as a seventh column, so that G^T X_p also yields g = G^T b'
-    if (sq < 12) {
-        const int w = sq / 6, i = sq % 6;
-        double ar[6], gm[28], xr[8];
-        const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
-        const double2* G2 = reinterpret_cast<const double2*>(CH.Gb[w]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) { const double2 v = A2[q]; ar[2 * q] = v.x; ar[2 * q + 1] = v.y; }
-#pragma unroll
-        for (int q = 0; q < 14; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double s2 = 0.0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) s2 += ar[k] * gm[k * 3 + j];            // G11
-#pragma unroll
-            for (int k = 0; k < 3; ++k) s2 += ar[3 + k] * gm[9 + k * 3 + j];   // G21
-            xr[j] = s2;
-            double s3 = 0.0;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) s3 += ar[3 + k] * gm[18 + k * 3 + j];  // G22
-            xr[3 + j] = s3;
-        }
-        xr[6] = w == 0 ? CH.B[i] : 0.0;
-        xr[7] = 0.0;
-        double2* X2 = reinterpret_cast<double2*>(CH.X[w][i]);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
-    }
-    wave_sync_lds();
-    // H = G_l^T X_r: eh = [Hpp upper 21 | Hgg upper 21 | Hgp 36 | gp 6 | gg 6].  Lane (T, i) < 9
-    // forms rows i and i + 3 of (T = 0) Gp^T [Xp | b'] -> Hpp, gp; (1) Gg^T [Xp | b'] -> Hgp, gg;
-    // (2) Gg^T Xg -> Hgg.  Row i < 3 takes G11 and G21, row i + 3 only G22 (zero block skipped).
-    if (sq < 9) {
-        const int T = sq / 3, i = sq % 3;
-        const double* Gl = CH.Gb[T == 0 ? 0 : 1];
-        const double2* X2 = reinterpret_cast<const double2*>(CH.X[T == 2 ? 1 : 0][0]);
-        double c11[3], c21[3], c22[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            c11[k] = Gl[k * 3 + i];
-            c21[k] = Gl[9 + k * 3 + i];
-            c22[k] = Gl[18 + k * 3 + i];
-        }
-        double h[7], h2[7];
-#pragma unroll
-        for (int j = 0; j < 7; ++j) { h[j] = 0.0; h2[j] = 0.0; }
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            double xk[8];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { const double2 v = X2[4 * k + q]; xk[2 * q] = v.x; xk[2 * q + 1] = v.y; }
-            const double c = k < 3 ? c11[k] : c21[k - 3];
-#pragma unroll
-            for (int j = 0; j < 7; ++j) h[j] += c * xk[j];
-            if (k >= 3) {
-#pragma unroll
-                for (int j = 0; j < 7; ++j) h2[j] += c22[k - 3] * xk[j];
-            }
-        }
-        double* out = a.eh + 90 * (size_t)eq;
-        const bool tri = T != 1;
-        const int i2 = i + 3;
-        const int blk = T == 2 ? 21 : 0;
-        double* o1 = tri ? out + blk + 6 * i - i * (i - 1) / 2 - i : out + 42 + 6 * i;
-        double* o2 = tri ? out + blk + 6 * i2 - i2 * (i2 - 1) / 2 - i2 : out + 42 + 6 * i2;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            if (!tri || j >= i) o1[j] = h[j];
-            if (!tri || j >= i2) o2[j] = h2[j];
-        }
-        if (T < 2) {
-            out[78 + 6 * T + i] = h[6];
-            out[78 + 6 * T + i2] = h2[6];
-        }
+        wave_sync_lds();
+        edge_chain_xh(CH, sq, eq, eq < a.n_edges, a);
     }
 #ifdef MCC_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2568,6 +2593,20 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 // last of the blocks and norm chunks adds the norms and, with fuse_solve (single GPU), solves.
 // (One last-arriver assembling every block alone took ~56 us at m = 90.)
 constexpr int kSub = 5;
+// entry tid < 48 of camera-pair block blk's sum -> the packed system (write-through)
+__device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, int tid, double v) {
+    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    int b1 = 0;
+    while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
+    const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
+    if (tid < 36) {
+        const int ii = tid / 6, jj = tid % 6;
+        if (b1 != b2 || ii <= jj) st_sc1(a.packed + packed_index(6 * b1 + ii, 6 * b2 + jj, m), v);
+    } else if (b1 == b2) {
+        const int w = (tid - 36) / 6, i = 6 * b1 + (tid - 36) % 6;
+        st_sc1(a.packed + ntri + w * m + i, v);   // r (w = 0), JTE of the global block (w = 1)
+    }
+}
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
 __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     State* st = a.state;
@@ -2578,8 +2617,8 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     __shared__ double part[kSub][48];
     __shared__ double red[256];
     if (item < a.n_items) {
-        const int4 it = a.items[item];   // {block, first slot's offset (doubles), slots, slot size 48 | 36}
-        const int q = tid % 48, sub = tid / 48, sz = it.w;
+        const int4 it = a.items[item];   // {block, first slot's offset (doubles), slots, slot size 48 | 36 [| single]}
+        const int q = tid % 48, sub = tid / 48, sz = it.w & (kItemSingle - 1);
         double s = 0.0;
         if (sub < kSub) {
             // the group sums k_photo wrote at the block's slots: independent coalesced loads,
@@ -2606,7 +2645,8 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         if (tid < 48) {
             double t = part[0][tid];
             for (int c = 1; c < kSub; ++c) t += part[c][tid];
-            st_sc1(a.item_out + 48 * (size_t)item + tid, t);
+            if (it.w & kItemSingle) schur_block_store(a, it.x, tid, 0.0 + t);   // as level 1 over one item
+            else st_sc1(a.item_out + 48 * (size_t)item + tid, t);
         }
     } else {
         const int c = item - a.n_items;
@@ -2626,14 +2666,11 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     // ---- level 1 (write-through hand-off, no fences): the last item of a camera-pair block sums
     // the block's items in item order and writes the block's entries of the packed system
-    if (item < a.n_items) {
+    if (item < a.n_items && !(a.items[item].w & kItemSingle)) {
         const int blk = a.items[item].x;
         const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
         if (!arrive_last_sc1(a.cnt_blk + blk, nk)) return;
         if (tid < 48) {
-            int b1 = 0;
-            while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
-            const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
             // unconditional loads (item_out is padded by kMaxItemsPerBlock zeroed items), masked adds
             double pv[kMaxItemsPerBlock];
 #pragma unroll
@@ -2641,13 +2678,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             double v = 0.0;
 #pragma unroll
             for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? pv[q] : 0.0;
-            if (tid < 36) {
-                const int ii = tid / 6, jj = tid % 6;
-                if (b1 != b2 || ii <= jj) st_sc1(a.packed + packed_index(6 * b1 + ii, 6 * b2 + jj, m), v);
-            } else if (b1 == b2) {
-                const int w = (tid - 36) / 6, i = 6 * b1 + (tid - 36) % 6;
-                st_sc1(a.packed + ntri + w * m + i, v);   // r (w = 0), JTE of the global block (w = 1)
-            }
+            schur_block_store(a, blk, tid, v);
         }
     }
     STAMPP(a.stamps, 8, 2);
@@ -2943,7 +2974,10 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
 
 // split step: lanes per edge of k_edge (88-corner edges: 6 passes at 92% lane use, the 27-value
 // butterfly over 16 lanes is a quarter of a wave's)
-constexpr int kEdgeLanes = 16;
+#ifndef MCC_EDGE_LANES
+#define MCC_EDGE_LANES 16
+#endif
+constexpr int kEdgeLanes = MCC_EDGE_LANES;   // lanes per edge in k_edge (16 or 8)
 template <int MODEL, bool RATIONAL, bool PRISM>
 static void launch_edge(const LinArgs& a, hipStream_t s) {
     constexpr int per = 64 / kEdgeLanes;
