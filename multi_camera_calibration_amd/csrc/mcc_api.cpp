@@ -727,8 +727,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->dg.alloc(p->m)); HIPC(p->delta.alloc(p->P));
     HIPC(p->photo_norm.alloc(2 * (size_t)V));
     if (p->fused) {
-        HIPC(p->contrib.alloc((size_t)p->packed_len * std::max(V, 1)));
-        HIPC(p->gsum.alloc((size_t)p->packed_len * p->n_groups));
+        // rows padded to an even count: 16-B write-through stores (k_linearize's hand-off)
+        const size_t lcp = (size_t)((p->packed_len + 1) & ~1);
+        HIPC(p->contrib.alloc(lcp * std::max(V, 1)));
+        HIPC(p->gsum.alloc(lcp * p->n_groups));
         HIPC(p->W.alloc((size_t)6 * p->m * std::max(V, 1)));
         HIPC(p->cnt.alloc(p->n_groups + 1));
         HIPC(hipMemset(p->cnt.p, 0, sizeof(int) * (p->n_groups + 1)));

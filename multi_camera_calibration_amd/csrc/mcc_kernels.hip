@@ -748,6 +748,15 @@ typedef __attribute__((address_space(1))) int gi32;
 __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// two doubles (16-B aligned) in one 16-B write-through store: MI355X_MICROARCH.md prices 8-B
+// `sc1` stores at 2.7x the per-byte time of 16-B ones (one fabric write per lane each)
+typedef double f64x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_sc1_x2(double* p, double a, double b) {
+    f64x2_t v;
+    v.x = a;
+    v.y = b;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 __device__ __forceinline__ double ld_sc1(const double* p) {
     return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
@@ -1239,11 +1248,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     // (k_schur's pair sums, src/multicalib.cpp:565-579 normal equations reduced onto the cameras)
     __syncthreads();
     STAMP(7);
-    const int m = a.global_dim, ntri = m * (m + 1) / 2, Lc = ntri + 2 * m + 2;
-    double* cv = a.contrib + (size_t)photo * Lc;
-    for (int t = tid; t < Lc; t += blockDim.x) {
+    const int m = a.global_dim, ntri = m * (m + 1) / 2, Lc = ntri + 2 * m + 2, Lcp = (Lc + 1) & ~1;
+    double* cv = a.contrib + (size_t)photo * Lcp;   // rows of Lcp (even): 16-B stores of value pairs
+    for (int tb = 0; tb < Lcp; tb += blockDim.x) {
+        const int t = tb + tid;
         double v = 0.0;
-        if (t < ntri) {
+        if (t >= Lc) {
+        } else if (t < ntri) {
             int i, j;
             packed_ij(t, m, i, j);
             const int bi = i / 6, bj = j / 6, ii = i % 6, jj = j % 6;
@@ -1277,7 +1288,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         } else {
             v = P.nrm[t - ntri - 2 * m];
         }
-        st_sc1(cv + t, v);
+        const double vn = dpp_f64<kDppXor1>(v);   // the odd partner's value (same wave)
+        if ((t & 1) == 0 && t < Lcp) st_sc1_x2(cv + t, v, vn);
     }
     STAMP(8);
     RSTAMP(29);
@@ -1298,10 +1310,11 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         return;
     }
     STAMP(9);
-    for (int t = tid; t < Lc; t += blockDim.x) {
-        double v = 0.0;
-        v = sum_sc1(a.contrib + (size_t)g0 * Lc + t, gn, Lc);
-        st_sc1(a.gsum + (size_t)grp * Lc + t, v);
+    for (int tb = 0; tb < Lcp; tb += blockDim.x) {
+        const int t = tb + tid;
+        const double v = t < Lc ? sum_sc1(a.contrib + (size_t)g0 * Lcp + t, gn, Lcp) : 0.0;
+        const double vn = dpp_f64<kDppXor1>(v);
+        if ((t & 1) == 0 && t < Lcp) st_sc1_x2(a.gsum + (size_t)grp * Lcp + t, v, vn);
     }
     STAMP(10);
     RSTAMP(30);
@@ -1330,7 +1343,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     const bool peer = a.peer.nranks > 0;
     for (int t = tid; t < Lc; t += blockDim.x) {
         double v = 0.0;
-        v = sum_sc1(a.gsum + t, a.n_groups, Lc);
+        v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
         if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
             const int w = t - ntri - 2 * m;
             if (iter0 > 0) {
@@ -1342,6 +1355,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         if (!peer) place(t, v);
         a.packed[t] = v;
     }
+    STAMP(17);   // thread 0's share of the assembly done (MCC_DIAG)
     if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
         if (!peer_exchange(a.peer, st, a.packed)) { RSTAMP(15); return; }
         for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);

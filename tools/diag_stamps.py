@@ -5,7 +5,7 @@ run time: read its shares.
 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_stamps.py [config] [views]
 
-Slots per workgroup (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written,
+Slots per workgroup (k_linearize): 0..7 s_memtime at phase boundaries, 8 contribution written, 17 final sum placed,
 9 group ticket won, 10 group sum written, 11 final ticket won, 12 system assembled, 13 solved
 (fused step); 14 / 15 s_memrealtime (100 MHz, chip-wide) at start / exit; 16, 18, 19 phase-0 detail
 (loads, back-solve, photo Rodrigues).  s_memtime is per XCD,
@@ -60,6 +60,7 @@ def main():
         if len(f):
             F = f[0]
             print(f"  final: ticket {F[11] - F[10]:.0f}, assemble {F[12] - F[11]:.0f}, solve {F[13] - F[12]:.0f}")
+            print(f"  assemble: thread 0's sum + placement {F[17] - F[11]:.0f}, then the barrier {F[12] - F[17]:.0f}")
             sv = F[20:27]
             print(f"  solve: stop test (wave 0) {sv[4] - sv[0]:.0f} incl. barrier; GJ (wave 1) {sv[2] - sv[1]:.0f}; "
                   f"after GJ -> update start {sv[5] - sv[4]:.0f}; update {sv[6] - sv[5]:.0f}; tail {F[13] - sv[6]:.0f}")
