@@ -1455,7 +1455,11 @@ __device__ __forceinline__ void prep_edge(const double* R1, const double* Jr1, c
     }
 }
 
-constexpr int kPrepGroup = 16;   // lanes per photo vertex in k_prep (4 photos per wave)
+#ifndef MCC_PREP_GROUP
+#define MCC_PREP_GROUP 16
+#endif
+constexpr int kPrepGroup = MCC_PREP_GROUP;   // lanes per photo vertex in k_prep (64 / kPrepGroup photos per wave)
+static_assert(kPrepGroup >= 8 && kPrepGroup <= 64 && (kPrepGroup & (kPrepGroup - 1)) == 0, "k_prep group");
 constexpr int kMaxEdgesPerPhoto = 64;   // split step (k_prep's LDS; mcc_create checks)
 #ifndef MCC_PREP_WAVES
 #define MCC_PREP_WAVES 2           // k_prep waves per SIMD
@@ -1600,7 +1604,7 @@ __global__ __launch_bounds__(64, MCC_PREP_WAVES) void k_prep(LinArgs a) {
     for (int le = l; le < ne; le += kPrepGroup) {
         const int e = e0 + le;
         int4 info = info0;
-        if (le >= kPrepGroup) {   // more than 16 edges: this edge's camera
+        if (le >= kPrepGroup) {   // more edges than lanes: this edge's camera
             info = a.edge_info[e];
             double om2[3];
             camera_pose_lds(s_cam, info.x, om2, T2);
