@@ -153,6 +153,7 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
     ba.timing_begin()
     ba.step(window)
     lin_ms, step_ms_ev, nlaunch = ba.timing_end()
+    ba.check()   # a failed step (peer timeout, not PD) stops the later ones: never report that as speed
     lin_ms = ba.allreduce_max(lin_ms)
     step_ms_ev = ba.allreduce_max(step_ms_ev)
     return dict(dt=dt, lin_ms=lin_ms, step_ms_ev=step_ms_ev, nlaunch=nlaunch,

@@ -112,6 +112,11 @@ int mcc_optimize(mcc_problem *p, int crit_type, int max_count, double eps, float
  * back-to-back calls only enqueue. */
 int mcc_step(mcc_problem *p, int n);
 int mcc_synchronize(mcc_problem *p);
+/* Wait for the enqueued steps, then report a device-side failure they hit (MCC_ECOMM: a peer
+ * exchange timed out; MCC_ENOTPD: a normal-equation block was not positive definite).  A
+ * failing step stops the free-running steps after it, so a throughput caller checks this once
+ * after its timed window (outside it: one small device-to-host copy). */
+int mcc_check(mcc_problem *p);
 
 /* computeProjectError(x): edge_err[E] (reference edge order, may be NULL), mean. */
 int mcc_project_error(mcc_problem *p, const float *x, float *edge_err, double *mean);

@@ -98,6 +98,7 @@ def lib():
                                    _i32p, _f64p]
         L.mcc_step.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.mcc_synchronize.argtypes = [ctypes.c_void_p]
+        L.mcc_check.argtypes = [ctypes.c_void_p]
         L.mcc_project_error.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f64p]
         L.mcc_debug_residuals.argtypes = [ctypes.c_void_p, _f32p, _f32p]
         L.mcc_timing_begin.argtypes = [ctypes.c_void_p]
@@ -274,6 +275,10 @@ class BundleAdjuster:
 
     def synchronize(self):
         _check(lib().mcc_synchronize(self.h), "mcc_synchronize")
+
+    def check(self):
+        """Raise if an enqueued step failed on the device (peer timeout, not positive definite)."""
+        _check(lib().mcc_check(self.h), "mcc_check")
 
     def residuals(self, x):
         x = np.ascontiguousarray(x, np.float32)

@@ -873,6 +873,14 @@ int mcc_synchronize(mcc_problem* p) {
     return MCC_OK;
 }
 
+int mcc_check(mcc_problem* p) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = read_state(p);
+    if (rc) return rc;
+    return check_state_error(p);
+}
+
 int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* mean) {
     if (!p || !x) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));

@@ -153,6 +153,7 @@ def test_step_flush(case):
     x_ref, _, it_ref, _ = o.optimize(p.x0, crit_type=1, max_count=n)
     g.set_params(p.x0)
     g.step(n)
+    g.check()   # free-running steps finished without a device-side failure
     x = g.get_params()
     assert it_ref == n
     assert f32_ulp_diff(x, x_ref).max() <= 1, name
@@ -160,6 +161,22 @@ def test_step_flush(case):
     d_ref, _ = o.linearize_solve(x_ref, "schur")
     d, _ = g.compute_jacobian_extrinsic(x)
     assert np.abs(d - d_ref).max() <= 1e-6 * np.abs(d_ref).max(), name
+
+
+def test_step_failure_is_reported(case):
+    """A step that fails on the device (NaN poses: the photo blocks are not positive definite)
+    stops the free-running steps after it; mcc_check reports it instead of a silently idle
+    stream (bench.py calls it after every timed window)."""
+    name, p, o, g = case
+    x = p.x0.astype(np.float32).copy()
+    x[:] = np.nan
+    g.set_params(x)
+    g.step(3)
+    with pytest.raises(api.MccError):
+        g.check()
+    g.set_params(p.x0)   # a fresh state clears the error
+    g.step(2)
+    g.check()
 
 
 # ---------------------------------------------------------------- committed golden fixtures
