@@ -590,7 +590,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // doubles; item = {block, first slot's offset, slots, slot size}
     int n_slots = 0;
     size_t n_doubles = 0;
-    int min_slots = 160;
+    int min_slots = 320;
     if (const char* f = std::getenv("MCC_ITEM_SLOTS")) min_slots = std::max(1, std::atoi(f));
     for (int b = 0; b < p->nblk; ++b) {
         int b1 = 0;
@@ -606,8 +606,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         if (n_doubles > (size_t)INT32_MAX) return bail(fail(MCC_EINVAL, "too many Schur pairs"));
         const int end = n_slots;
         // <= 24 work items per block keeps the last-arriver assembly short; >= min_slots slots per
-        // item (MCC_ITEM_SLOTS, default 160) amortises an item's fixed latency (one load round trip, the
-        // write-through hand-off and ticket) over more slots
+        // item (MCC_ITEM_SLOTS, default 320) amortises an item's fixed latency (one load round trip, the
+        // write-through hand-off and ticket) over more slots (config3, interleaved: 160 -> 320 slots
+        // 120.8 -> 119.6 us per step, 640 122.3; configs 4 and 5 within noise)
         // A block of at most min_slots slots is one item, which writes the block's packed entries
         // itself (slot size | kItemSingle): no item hand-off level (config4: every block, k_schur
         // 9.2 -> 8.7 us).  Larger blocks keep >= min_slots per item: config5's one block of 250

@@ -2626,6 +2626,9 @@ __device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, i
     }
 }
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
+#ifndef MCC_SCHUR_LOADS
+#define MCC_SCHUR_LOADS 32
+#endif
 __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
@@ -2642,10 +2645,10 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             // the group sums k_photo wrote at the block's slots: independent coalesced loads,
             // eight in flight per thread (entries >= 36 of an off-diagonal block: none, zeros)
             if (q < sz) {
-                // slots sub, sub + kSub, ... summed in that order; 32 loads per thread in flight per
-                // round (one round for the host's items of <= 160 slots)
+                // slots sub, sub + kSub, ... summed in that order; MCC_SCHUR_LOADS loads per thread in
+                // flight per round (the summation order does not depend on it)
                 const double* pp = a.pairprod + (size_t)it.y + q;
-                constexpr int U = 32;
+                constexpr int U = MCC_SCHUR_LOADS;
                 for (int p0 = sub; p0 < it.z; p0 += U * kSub) {
                     double v[U];
 #pragma unroll
