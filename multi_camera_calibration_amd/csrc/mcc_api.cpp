@@ -613,8 +613,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         // itself (slot size | kItemSingle): no item hand-off level (config4: every block, k_schur
         // 9.2 -> 8.7 us).  Larger blocks keep >= min_slots per item: config5's one block of 250
         // slots as a single item took 10.7 us against 9.3 as two items and the hand-off.
-        const int per_item = std::max(min_slots, (end - begin + 23) / 24);
-        const int single = (end - begin <= per_item) ? mcc::kItemSingle : 0;
+        // Blocks of (single_max, min_slots] slots take two items (config5's 250-slot block: k_schur
+        // 10.5 us as one item vs 9.8 as two under rocprofv3)
+        const int nsl = end - begin, single_max = std::min(min_slots, 160);
+        int per_item = std::max(min_slots, (nsl + 23) / 24);
+        if (nsl > single_max && nsl <= per_item) per_item = (nsl + 1) / 2;
+        const int single = (nsl <= per_item) ? mcc::kItemSingle : 0;
         for (int s = begin; s < end; s += per_item)
             items.push_back(make_int4(b, (int)(base + (size_t)(s - begin) * stride), std::min(end, s + per_item) - s,
                                       stride | single));
