@@ -1,29 +1,33 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X BA hot path (one Gauss-Newton step of optimizeExtrinsics).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config config2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config config4]
 
 One "step" = one pass of the hot path over the whole problem: linearisation of every corner
 (residual + Jacobian), normal-equation reduction, Schur solve, float32 update
 (MultiCameraCalibration::optimizeExtrinsics loop body, src/multicalib.cpp:481-506).
 
-Headline workload: BASELINE.json configs[1] (4 pinhole cameras, 500 synthetic 11x8-board views)
-per rank.  N > 1 ranks (one process per GPU, launched by torch.distributed.run) weak-scale it: the
-rig has 500*N views, photo vertices are sharded and each step exchanges the reduced camera system
-once: over the peer transport (mcc_peer_*: the final arriving workgroup of each rank writes its
-system into every peer's inbox over xGMI and solves, one kernel per step) when the handshake
-passes on every rank, else with one RCCL all-reduce (MCC_TRANSPORT=rccl forces it).
+Headline workload (N = 1): BASELINE.json configs[3] -- 4 omnidirectional cameras, 1 000 synthetic
+11x8-board views -- the largest BASELINE config quoted on one MI355X; configs[1] (4 pinhole
+cameras, 500 views) is reported at the same level under "configs" (with configs 3 and 5).
+N > 1 ranks (one process per GPU, launched by torch.distributed.run) weak-scale the headline
+workload: the rig has 1 000*N views, photo vertices are sharded and each step exchanges the reduced
+camera system once: over the peer transport (mcc_peer_*: the final arriving workgroup of each rank
+writes its system into every peer's inbox over xGMI and solves) when the handshake passes on
+every rank, else with one RCCL all-reduce (MCC_TRANSPORT=rccl forces it).
 
 Timing: an untimed clock ramp (>= --ramp-seconds of steps, the same step count on every rank),
-W warmup steps, then exactly K steps between barriers (max over ranks); the dominant kernel is
-then timed with HIP events over a window of max(100, K) further launches.
+W warmup steps, then exactly K steps between barriers (max over ranks); the dominant kernel(s)
+are then timed with HIP events over a window of max(100, K) further launches.
 
 Extra keys (same JSON line):
-  * N = 1: "configs" -- configs 3, 4 and 5 of BASELINE.json at full size on this GPU (ms per
-    step, corner evals/s, k_linearize time and HBM-roofline fraction);
+  * N = 1: "configs" -- the other BASELINE configs (2, 3, 5) at full size on this GPU (ms per
+    step, corner evals/s, linearisation time and HBM-roofline fraction, traffic and FP64 from the
+    committed rocprofv3 summaries);
   * N > 1: "strong" -- the BASELINE multi-GPU rigs at their fixed size split over the N ranks
     (config3: 16 cameras x 5k views; config5: 8-camera double-sided board x 2k views), the
-    strong-scaling curve north_star names;
+    strong-scaling curve north_star names, with BOTH transports (peer and RCCL) and each one's
+    per-step exchange time;
   * "cpu_baseline" (the OpenMP Schur port on the same workload) and "cpu_baseline_ref_faithful"
     (the reference's own algorithm -- dense J, J^T J, Jacobi-CG x2 -- single-threaded on config1).
 
@@ -153,10 +157,12 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
     ba.timing_begin()
     ba.step(window)
     lin_ms, step_ms_ev, nlaunch = ba.timing_end()
+    xchg_ms, n_xchg = ba.timing_exchange()
     ba.check()   # a failed step (peer timeout, not PD) stops the later ones: never report that as speed
     lin_ms = ba.allreduce_max(lin_ms)
     step_ms_ev = ba.allreduce_max(step_ms_ev)
-    return dict(dt=dt, lin_ms=lin_ms, step_ms_ev=step_ms_ev, nlaunch=nlaunch,
+    xchg_ms = ba.allreduce_max(xchg_ms)
+    return dict(dt=dt, lin_ms=lin_ms, step_ms_ev=step_ms_ev, nlaunch=nlaunch, xchg_ms=xchg_ms, n_xchg=n_xchg,
                 ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)})
 
 
@@ -180,6 +186,18 @@ def roofline(st, lin_ms, tr=None, kernel="k_linearize"):
         "alg_bytes_formula": "20 B/corner (float32 obj xyz + img uv) + 280 B/edge (SURVEY.md 8(d))",
         "kernel_ms_per_launch": lin_ms,
     }
+
+
+MODEL_NAMES = {rig.PINHOLE: "pinhole", rig.OMNI: "omnidirectional", rig.DOUBLESIDE: "double-sided-board pinhole"}
+CONFIG_INDEX = {"config1": 0, "config2": 1, "config3": 2, "config4": 3, "config5": 4}
+
+
+def workload_label(name: str, views_per_rank: int, world: int) -> str:
+    c = rig.CONFIGS[name]
+    board = "x".join(map(str, c["board"]))
+    per = " per rank" if world > 1 else ""
+    return (f"{name}: {c['n_cams']} {MODEL_NAMES[c['model']]} cameras, {views_per_rank} synthetic {board}-board "
+            f"views{per} (BASELINE.json configs[{CONFIG_INDEX[name]}]), one Gauss-Newton step per 'step'")
 
 
 def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
@@ -211,22 +229,33 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
 
 
 def strong_line(name: str, rank: int, world: int, local_rank: int, same_device: bool, steps: int = 100):
-    """A BASELINE multi-GPU rig at its fixed size, photo vertices split over the ranks."""
+    """A BASELINE multi-GPU rig at its fixed size, photo vertices split over the ranks; timed with
+    the peer transport and with RCCL (the same problem, mcc_peer_enable toggles), each with its
+    per-step exchange time (mcc_timing_exchange: in-kernel ticks / HIP events around the
+    all-reduce)."""
     full = rig.make_config(name)
     owner = api.partition_photos(full, world)
     prob = rig.subset_photos(full, np.nonzero(owner == rank)[0])
     ba = api.BundleAdjuster(prob, device=0 if same_device else local_rank)
+    out = {"views": full.n_photos, "cameras": full.n_cams, "corners_per_step": full.n_corners,
+           "unit": "corner evals/s", "n_gpus": world, "scaling": "strong"}
     try:
-        transport = setup_transport(ba, rank, world, same_device, f"strong_{name}")
-        ba.set_params(prob.x0)
-        m = measure(ba, steps, 10, 0.15, max(100, steps))
+        first = setup_transport(ba, rank, world, same_device, f"strong_{name}")
+        order = [first] + ([t for t in ("peer", "rccl") if t != first and first == "peer"] if not same_device else [])
+        for tr in order:
+            if not same_device:
+                ba.peer_enable(tr == "peer")
+            ba.set_params(prob.x0)
+            m = measure(ba, steps, 10, 0.15, max(100, steps))
+            ms = m["dt"] / steps * 1e3
+            out[tr] = {"value": full.n_corners / (ms * 1e-3), "ms_per_step": ms,
+                       "kernel_ms_per_launch": m["lin_ms"], "step_ms_events": m["step_ms_ev"],
+                       "exchange_ms": m["xchg_ms"], "exchanges_timed": m["n_xchg"]}
     finally:
         ba.close()
-    ms = m["dt"] / steps * 1e3
-    return {"views": full.n_photos, "cameras": full.n_cams, "corners_per_step": full.n_corners,
-            "value": full.n_corners / (ms * 1e-3), "unit": "corner evals/s", "ms_per_step": ms,
-            "n_gpus": world, "transport": transport, "kernel_ms_per_launch": m["lin_ms"],
-            "step_ms_events": m["step_ms_ev"], "scaling": "strong"}
+    best = min((t for t in ("peer", "rccl") if t in out), key=lambda t: out[t]["ms_per_step"])
+    out.update(value=out[best]["value"], ms_per_step=out[best]["ms_per_step"], transport=best)
+    return out
 
 
 def cpu_baseline(prob, target_s: float):
@@ -276,7 +305,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="config2")
+    ap.add_argument("--config", default="config4")
     ap.add_argument("--views", type=int, default=None, help="views per rank (default: the config's)")
     ap.add_argument("--ramp-seconds", type=float, default=0.25, help="untimed clock ramp before the warmup")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -320,6 +349,7 @@ def main():
     if rank != 0:
         return
     tr = load_profile("traffic", args.config, views_per_rank) if world == 1 else None
+    model = MODEL_NAMES[rig.CONFIGS[args.config]["model"]]
     rl = roofline(st, m["lin_ms"], tr, kernel=kern)
     rl["kernel_launches_timed"] = m["nlaunch"]
     rl["step_ms_events"] = m["step_ms_ev"]
@@ -337,9 +367,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": f"{args.config}: {full.n_cams} pinhole cameras, {views_per_rank} synthetic "
-                        f"{'x'.join(map(str, rig.CONFIGS[args.config]['board']))}-board views per rank "
-                        f"(BASELINE.json configs[1]), one Gauss-Newton step per 'step'",
+            "workload": workload_label(args.config, views_per_rank, world),
+            "model": model,
             "cameras": full.n_cams, "views": full.n_photos, "edges": full.n_edges,
             "corners_per_step": int(corners_total), "params": full.n_params,
             "parallelism": f"photo-sharded x{world}" + (
@@ -349,6 +378,7 @@ def main():
             "state_dtype": "f32", "jacobian_dtype": "f64",
         },
         "clock_ramp": m["ramp"],
+        "exchange_ms": m["xchg_ms"] if world > 1 else None,
         "roofline": rl,
     }
     fp = load_profile("fp64", args.config, views_per_rank) if world == 1 else None
@@ -372,7 +402,8 @@ def main():
                          "iters_gpu": itg, "iters_oracle": itr,
                          "max_abs_param_diff": float(np.abs(xg - xr).max())}
     if world == 1 and not args.no_extra:
-        out["configs"] = {name: config_line(name, device=local_rank) for name in ("config3", "config4", "config5")}
+        out["configs"] = {name: config_line(name, device=local_rank)
+                          for name in ("config2", "config3", "config4", "config5") if name != args.config}
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(prob, args.cpu_seconds)
         out["cpu_baseline_ref_faithful"] = cpu_baseline_ref_faithful()

@@ -114,8 +114,12 @@ int mcc_step(mcc_problem *p, int n);
 int mcc_synchronize(mcc_problem *p);
 /* Wait for the enqueued steps, then report a device-side failure they hit (MCC_ECOMM: a peer
  * exchange timed out; MCC_ENOTPD: a normal-equation block was not positive definite).  A
- * failing step stops the free-running steps after it, so a throughput caller checks this once
- * after its timed window (outside it: one small device-to-host copy). */
+ * failing step sets the device loop's stop flag (the final solve of the step does, or the peer
+ * exchange on a timeout), so the free-running steps after it are no-ops; a throughput caller
+ * checks this once after its timed window (outside it: one small device-to-host copy).  The
+ * error stays in the device state until an entry point rewrites it (mcc_set_params,
+ * mcc_optimize, mcc_linearize_solve); after mcc_check has reported it, the next mcc_step also
+ * rewrites it and continues from the current parameters. */
 int mcc_check(mcc_problem *p);
 
 /* computeProjectError(x): edge_err[E] (reference edge order, may be NULL), mean. */
@@ -162,6 +166,11 @@ int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
  * pair around the k_prep + k_edge + k_photo launches of every step (eager). */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
+/* average time (ms) of the step's data-path exchange over the same window, and the exchanges:
+ * RCCL all-reduces by HIP event pairs around each ncclAllReduce, the peer transport by the
+ * device's own s_memrealtime ticks from the first send to the rank-ordered sums (in-kernel, so
+ * it includes waiting for the slowest rank).  0 exchanges on a single rank. */
+int mcc_timing_exchange(mcc_problem *p, double *ms_per_exchange, int *exchanges);
 /* diagnostic build only (libmcc_diag.so, -DMCC_DIAG): first call arms per-phase s_memtime
  * stamps (k_linearize; split step: k_photo per group, k_prep, k_edge rows), later calls copy
  * [32 * n_photos] stamps (then k_schur's [8 * grid]) out
@@ -172,7 +181,10 @@ int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges
                       long long *photos, long long *alg_bytes_per_step);
 /* which step the problem runs: *split_step = 0 for the fused single-kernel step (m <= 30 and at
  * most two photo workgroups per CU, or MCC_FUSED=1), 1 for the split step (k_prep, k_edge,
- * k_photo, k_schur, k_solve); *photo_groups = k_photo's workgroups (split step) */
+ * k_photo, k_schur, k_solve); *photo_groups = k_photo's workgroups (split step).  The choice
+ * depends on the device's CU count (fused iff m <= 30 and n_photos <= 2 x CUs: 512 on MI355X), and
+ * the two paths sum the normal equations in different orders, so the last FP64 bits of a step (and
+ * in rare cases a float32 ulp of the state) depend on the device model; MCC_FUSED pins it. */
 int mcc_problem_path(const mcc_problem *p, int *split_step, int *photo_groups);
 
 #ifdef __cplusplus

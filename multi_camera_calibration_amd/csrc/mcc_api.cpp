@@ -202,6 +202,13 @@ struct mcc_problem {
     bool timing_window = false;
     hipEvent_t ev_win[2] = {nullptr, nullptr};
     long long win_steps = 0;
+    // exchange time over the window: RCCL all-reduces by event pairs (eager window), the peer
+    // exchange by the device's own tick sum (State::xchg_ticks, in-kernel) against its value and
+    // the epoch at mcc_timing_begin
+    std::vector<hipEvent_t> ev_x;
+    int ev_x_used = 0;
+    long long xchg_ticks0 = 0;
+    unsigned xchg_epoch0 = 0;
 };
 
 namespace {
@@ -273,9 +280,15 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
     if (p->fused) {
         if (rccl) {
+            const bool tx = tim && p->ev_x_used + 2 <= (int)p->ev_x.size();
+            if (tx) HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used], p->stream));
             ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                            p->comm, p->stream);
             if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+            if (tx) {
+                HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used + 1], p->stream));
+                p->ev_x_used += 2;
+            }
             SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false)};
             HIPCHK(mcc_launch_solve(so, p->stream));
         }
@@ -305,9 +318,15 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
     if (rccl) {
+        const bool tx = tim && p->ev_x_used + 2 <= (int)p->ev_x.size();
+        if (tx) HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used], p->stream));
         ncclResult_t r = ncclAllReduce(p->packed.p, p->packed.p, (size_t)p->packed_len, ncclDouble, ncclSum,
                                        p->comm, p->stream);
         if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        if (tx) {
+            HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used + 1], p->stream));
+            p->ev_x_used += 2;
+        }
     }
     if (split) {
         SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer)};
@@ -767,6 +786,7 @@ void mcc_destroy(mcc_problem* p) {
         if (g) (void)hipGraphExecDestroy(g);
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
+    for (auto e : p->ev_x) (void)hipEventDestroy(e);
     for (auto e : p->ev_win) if (e) (void)hipEventDestroy(e);
     if (p->comm) (void)ncclCommDestroy(p->comm);
     for (void* m : p->peer_mapped) (void)hipIpcCloseMemHandle(m);
@@ -883,7 +903,11 @@ int mcc_check(mcc_problem* p) {
     HIPCHK(hipSetDevice(p->device));
     int rc = read_state(p);
     if (rc) return rc;
-    return check_state_error(p);
+    rc = check_state_error(p);
+    // a failed step left `done` set: the next mcc_step must rewrite the state (set_state), not
+    // enqueue onto a stopped loop
+    if (rc) p->stepping = false;
+    return rc;
 }
 
 int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* mean) {
@@ -964,6 +988,17 @@ int mcc_timing_begin(mcc_problem* p) {
         for (auto& e : p->ev_step) HIPCHK(hipEventCreate(&e));
     }
     p->ev_used = 0;
+    p->ev_x_used = 0;
+    if (p->ev_x.empty()) {
+        p->ev_x.resize(512);
+        for (auto& e : p->ev_x) HIPCHK(hipEventCreate(&e));
+    }
+    {
+        int rc = read_state(p);
+        if (rc) return rc;
+        p->xchg_ticks0 = p->h_state->xchg_ticks;
+        p->xchg_epoch0 = p->h_state->epoch;
+    }
     if (p->fused && (!p->comm || p->peer_on)) {   // one kernel per step: time the launch window itself (graphs stay on)
         if (!p->ev_win[0]) {
             HIPCHK(hipEventCreate(&p->ev_win[0]));
@@ -1006,6 +1041,29 @@ int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launche
     if (lin_ms) *lin_ms = n ? lin / n : 0.0;
     if (step_ms) *step_ms = n ? st / n : 0.0;
     if (launches) *launches = n;
+    return MCC_OK;
+}
+
+int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipSetDevice(p->device));
+    int rc = read_state(p);
+    if (rc) return rc;
+    double ms = 0.0;
+    int n = 0;
+    if (p->peer_on) {
+        n = (int)(p->h_state->epoch - p->xchg_epoch0);
+        ms = (double)(p->h_state->xchg_ticks - p->xchg_ticks0) * 1e-5;   // 100 MHz ticks -> ms
+    } else {
+        n = p->ev_x_used / 2;
+        for (int i = 0; i < n; ++i) {
+            float a = 0;
+            HIPCHK(hipEventElapsedTime(&a, p->ev_x[2 * i], p->ev_x[2 * i + 1]));
+            ms += a;
+        }
+    }
+    if (ms_per_exchange) *ms_per_exchange = n ? ms / n : 0.0;
+    if (exchanges) *exchanges = n;
     return MCC_OK;
 }
 

@@ -22,6 +22,7 @@ struct State {
     int error;        // bit 0: photo block not PD, bit 1: camera system not PD, bit 2: peer timeout
     int pending;      // a solved photo update waits to be applied by the next k_linearize
     unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
+    long long xchg_ticks; // s_memrealtime ticks (100 MHz) inside peer exchanges, summed (monotonic)
 };
 
 // Peer transport (multi-GPU without RCCL in the step): every rank's final arriver writes its packed

@@ -849,6 +849,7 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
     __shared__ unsigned ep_s;
     __shared__ int to_s;
     const int tid = threadIdx.x;
+    const long long tx0 = (long long)__builtin_amdgcn_s_memrealtime();   // exchange time (thread 0's)
     if (tid == 0) {
         ep_s = st->epoch + 1u;
         to_s = 0;
@@ -863,6 +864,7 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
     __syncthreads();
     if (tid == 0) {
         st->epoch = ep;
+        st->xchg_ticks += (long long)__builtin_amdgcn_s_memrealtime() - tx0;   // mcc_timing_exchange
         if (to_s) {
             st->error |= 4;
             st->done = 1;
@@ -2596,6 +2598,12 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
             st->pending = 1;
         }
     }
+    // a step that hit a not-positive-definite block (a photo's: bit 0, set by the photo workgroups
+    // before their tickets; the reduced system's: bit 1, set by this workgroup's elimination) stops
+    // the steps after it, as mcc_check documents; the kernels test `done` only at their entry, so
+    // no launch in flight loses a workgroup's ticket
+    __syncthreads();
+    if (tid == 0 && (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3)) st->done = 1;
 }
 
 // ---------------------------------------------------------------- k_schur

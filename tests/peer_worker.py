@@ -51,7 +51,8 @@ def main():
     ba.peer_init(handles, world, rank)
     mx = ba.allreduce_max(rank + 0.5)
     d, j = ba.compute_jacobian_extrinsic(q.x0)
-    x, _, it, ch = ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=1e-7)
+    eps = 1e-8 if q.model == rig.DOUBLESIDE else 1e-7   # doubleSide.hpp:105 / mymulticalib.hpp:96
+    x, _, it, ch = ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=eps)
     # throughput of unconditional steps (the bench's loop) over the transport
     ba.set_params(q.x0)
     ba.step(10)

@@ -252,27 +252,58 @@ def test_repeatable_bitwise():
         g.close()
 
 
-def test_unobserved_camera_not_pd():
+@pytest.mark.parametrize("name,views,cam,split", [
+    ("config2", 30, 3, False),   # fused step: the final arriver's register elimination
+    ("config2", 30, 3, True),    # split step: k_schur's empty kItemSingle items write the zero block
+    ("config3", 60, 7, True),    # m = 90: k_solve's blocked factorisation
+])
+def test_unobserved_camera_not_pd(name, views, cam, split):
     """A camera no photo observes is accepted by mcc_create (a photo shard of a multi-GPU problem
     may lack one, tests/test_peer_transport.py config2_nocam); on a whole problem its block of the
-    reduced system is zero and the solve fails loudly with MCC_ENOTPD instead of returning a step."""
-    p = rig.make_config("config2", n_views=30)
-    keep = np.setdiff1d(np.arange(p.n_photos), np.unique(p.edge_photo[p.edge_cam == 3]))
+    reduced system is zero and the solve fails loudly with MCC_ENOTPD instead of returning a step,
+    on every solve path.  The failed step also stops the free-running steps after it (mcc_check),
+    and a fresh state clears the error."""
+    p = rig.make_config(name, n_views=views)
+    keep = np.setdiff1d(np.arange(p.n_photos), np.unique(p.edge_photo[p.edge_cam == cam]))
     q = rig.subset_photos(p, keep)
-    assert q.n_cams == 4 and not np.any(q.edge_cam == 3)
-    g = api.BundleAdjuster(q)
+    assert q.n_cams == p.n_cams and not np.any(q.edge_cam == cam)
+    g = make_adjuster(name + ("_split" if split else ""), q)
     try:
+        assert g.path() == ("split" if split else "fused")
         with pytest.raises(api.MccError, match="not positive definite"):
             g.compute_jacobian_extrinsic(q.x0)
+        g.set_params(q.x0)
+        g.step(3)
+        with pytest.raises(api.MccError, match="not positive definite"):
+            g.check()
     finally:
         g.close()
+
+
+def _device_cus():
+    """Compute units of the GPU the tests run on (rocminfo), the bound of the fused path's rule."""
+    import re
+    import subprocess
+    try:
+        out = subprocess.run(["rocminfo"], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                             timeout=60).stdout
+    except (OSError, subprocess.TimeoutExpired):
+        return 256
+    for agent in out.split("Agent ")[1:]:
+        if "gfx" in agent:
+            m = re.search(r"Compute Unit:\s+(\d+)", agent)
+            if m:
+                return int(m.group(1))
+    return 256
 
 
 def test_step_path_selection():
     """mcc_create's choice (mcc_problem_path): the fused single-kernel step for m <= 30 with at most
     two photo workgroups per CU, the split step for more photos or m > 30; MCC_FUSED=0 forces the
-    split step (the *_split cases above)."""
-    cases = [("config2", 500, "fused"), ("config2", 1200, "split"), ("config3", 40, "split"), ("config5", 60, "fused")]
+    split step (the *_split cases above).  The photo bound follows the device's CU count."""
+    cus = _device_cus()
+    cases = [("config2", 2 * cus, "fused"), ("config2", 2 * cus + 64, "split"), ("config3", 40, "split"),
+             ("config5", 60, "fused")]
     for name, views, want in cases:
         p = rig.make_config(name, n_views=views)
         g = api.BundleAdjuster(p)
