@@ -167,9 +167,9 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
 
 
 def lin_kernels(ba) -> str:
-    """The kernels of the linearisation window (mcc_timing_*): the fused kernel, or the split
-    step's three (mcc_problem_path says which the problem runs)."""
-    return "k_prep+k_edge+k_photo" if ba.path() == "split" else "k_linearize"
+    """The kernels of the linearisation window (mcc_timing_*): the fused kernel, the split step's
+    group kernel, or its three-kernel form (mcc_problem_path says which)."""
+    return ba.step_kernels()
 
 
 def roofline(st, lin_ms, tr=None, kernel="k_linearize"):

@@ -323,6 +323,14 @@ class BundleAdjuster:
         _check(lib().mcc_problem_path(self.h, ctypes.byref(sp), ctypes.byref(ng)), "mcc_problem_path")
         return "split" if sp.value else "fused"
 
+    def step_kernels(self):
+        """The kernels of one step's linearisation: 'k_linearize' (fused), 'k_group' (the split step's
+        fused group kernel) or 'k_prep+k_edge+k_photo' (MCC_GROUP=0)."""
+        sp = ctypes.c_int(0)
+        ng = ctypes.c_int(0)
+        _check(lib().mcc_problem_path(self.h, ctypes.byref(sp), ctypes.byref(ng)), "mcc_problem_path")
+        return {0: "k_linearize", 1: "k_prep+k_edge+k_photo", 2: "k_group"}[sp.value]
+
     def stamps(self):
         """libmcc_diag.so only: first call arms, later calls return [n_photos, 32] s_memtime stamps
         followed by k_schur's [workgroups, 8]."""

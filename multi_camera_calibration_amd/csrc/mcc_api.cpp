@@ -142,6 +142,10 @@ struct mcc_problem {
     // split step's k_photo groups (consecutive photos) and their pair / contribution lists
     int n_pgroups = 0, max_gpairs = 0, max_gcon = 0, max_gedges = 0;
     size_t photo_shmem = 0;
+    // split step as ONE fused kernel per group (k_group: photo update, edge prologues, sweep, chain,
+    // photo Schur work) instead of k_prep -> k_edge -> k_photo; MCC_GROUP=0 selects the three
+    int use_group = 1;
+    size_t group_shmem = 0;
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
@@ -272,7 +276,9 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.n_edges = p->E; la.n_photos = p->V;
     la.erec = p->erec.p; la.echain = p->echain.p; la.eh = p->eh.p;
     if (p->V > 0) {
-        if (!p->fused)
+        if (!p->fused && p->use_group)
+            HIPCHK(mcc_launch_group(la, p->model, p->rational, p->prism, p->group_shmem, p->stream));
+        else if (!p->fused)
             HIPCHK(mcc_launch_split(la, p->model, p->rational, p->prism, p->photo_shmem, p->stream));
         else
             HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
@@ -540,25 +546,50 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         p->max_cpp = std::max(p->max_cpp, photo_corner[v + 1] - photo_corner[v]);
     }
 
-    // ---- Schur pair lists.  k_photo (split step) takes groups of consecutive photos (at most
-    // kPhotoGroup photos / kPhotoGroupEdges edges) and sums the group's pair products per
-    // camera-pair block: one slot per (group, block), block-major over the groups, k_schur sums a
-    // block's slots in order.  A contribution is one ordered edge pair (e1, e2) of a photo with
-    // gblock(e1) <= gblock(e2) (both orders within one block), in photo then edge order.
+    // small camera blocks and at most two photo workgroups per CU (the fused kernel's occupancy):
+    // one kernel per Gauss-Newton step.  More photos than that run the fused kernel's serial
+    // per-photo chain in several rounds, and the split step is faster (config4, 1000 views:
+    // 43.3 vs 47.4 us; config2, 500 views: 38.2 vs 25.9 us).  MCC_FUSED=1 / 0 forces either.
+    int n_cu = 256;
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
+        n_cu = 256;
+    const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
+    p->fused = fusable && V <= 2 * n_cu;
+    if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
+    if (!p->fused && p->max_epp > 64)
+        return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
+
+    // ---- Schur pair lists.  The split step's photo work (k_group / k_photo) takes groups of
+    // consecutive photos (at most kPhotoGroup photos and the cap's edges) and sums the group's pair
+    // products per camera-pair block: one slot per (group, block), block-major over the groups,
+    // k_schur sums a block's slots in order.  A contribution is one ordered edge pair (e1, e2) of a
+    // photo with gblock(e1) <= gblock(e2) (both orders within one block), in photo then edge order.
     const int nb = p->m / 6;
     p->nblk = nb * (nb + 1) / 2;
     auto blk_index = [nb](int b1, int b2) { return b1 * nb - b1 * (b1 - 1) / 2 + (b2 - b1); };
-    std::vector<int> pgrp_ptr(1, 0);
-    for (int v = 0; v < V;) {
-        int w = v, edges = 0;
-        while (w < V && w - v < mcc::kPhotoGroup &&
-               (w == v || edges + (photo_ptr[w + 1] - photo_ptr[w]) <= mcc::kPhotoGroupEdges)) {
-            edges += photo_ptr[w + 1] - photo_ptr[w];
-            ++w;
+    auto make_groups = [&](int cap) {
+        std::vector<int> g(1, 0);
+        for (int v = 0; v < V;) {
+            int w = v, edges = 0;
+            while (w < V && w - v < mcc::kPhotoGroup &&
+                   (w == v || edges + (photo_ptr[w + 1] - photo_ptr[w]) <= cap)) {
+                edges += photo_ptr[w + 1] - photo_ptr[w];
+                ++w;
+            }
+            g.push_back(w);
+            v = w;
         }
-        pgrp_ptr.push_back(w);
-        v = w;
-    }
+        return g;
+    };
+    // k_group takes groups of at most kGroupRound edges (one 16-edge round per workgroup; config4's
+    // 1 000 photos -> 250 workgroups, one per CU); k_photo's groups sum more photos (<= 64 edges).
+    // k_group (two workgroups per CU) wins while its groups fit the CUs in one wave of workgroups
+    // (config4: 32.3 vs 36.9 us per step); with more groups the three-kernel form's higher
+    // occupancy wins (config5: 67.3 vs 61.0, config3: 185.5 vs 120.5).  MCC_GROUP=1 / 0 forces.
+    std::vector<int> pgrp_ptr = make_groups(mcc::kGroupRound);
+    p->use_group = !p->fused && (int)pgrp_ptr.size() - 1 <= n_cu;
+    if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
+    if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);
     const int NG = (int)pgrp_ptr.size() - 1;
     std::vector<int4> gpairs;                           // {first contribution, count, diagonal << 1, slot}
     std::vector<unsigned> gcon;
@@ -602,6 +633,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     }
     p->n_pgroups = NG;
     p->photo_shmem = mcc::photo_lds_bytes(p->max_gedges, p->max_gpairs, p->max_gcon);
+    p->group_shmem = mcc::group_lds_bytes(p->max_gedges, C, p->max_gpairs, p->max_gcon);
     std::vector<int4> items;
     std::vector<int> block_items(p->nblk + 1, 0);
     // slot sizes: 48 doubles on a diagonal camera-pair block (S entries, r, JTE), 36 off the
@@ -655,18 +687,6 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
-    // small camera blocks and at most two photo workgroups per CU (the fused kernel's occupancy):
-    // one kernel per Gauss-Newton step.  More photos than that run the fused kernel's serial
-    // per-photo chain in several rounds, and the split step is faster (config4, 1000 views:
-    // 43.3 vs 47.4 us; config2, 500 views: 38.2 vs 25.9 us).  MCC_FUSED=1 / 0 forces either.
-    int n_cu = 256;
-    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
-        n_cu = 256;
-    const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
-    p->fused = fusable && V <= 2 * n_cu;
-    if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
-    if (!p->fused && p->max_epp > 64)
-        return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;
 
@@ -732,7 +752,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(p->x.alloc(p->P)); HIPC(p->xerr.alloc(p->P));
     HIPC(p->Y.alloc(36 * (size_t)E));
     HIPC(p->pairprod.alloc(p->fused ? 0 : p->n_pair_doubles));
-    const bool use_split = !p->fused;
+    const bool use_split = !p->fused && !p->use_group;   // k_prep -> k_edge -> k_photo records
     HIPC(p->erec.alloc(use_split ? 12 * (size_t)E : 0));
     HIPC(p->echain.alloc(use_split ? 54 * (size_t)E : 0));
     HIPC(p->eh.alloc(use_split ? 90 * (size_t)E : 0));
@@ -769,9 +789,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (C > 63) return bail(fail(MCC_EINVAL, "more than 63 cameras"));
     if (p->fused && mcc_lin_shmem(p->max_epp, C, p->m, p->max_cpp) > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many edges / corners per photo for the LDS staging"));
-    if (!p->fused && p->photo_shmem > 160 * 1024)
+    if (!p->fused && !p->use_group && p->photo_shmem > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many Schur pairs of one photo for k_photo's LDS"));
-    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem));
+    if (!p->fused && p->use_group && p->group_shmem > 160 * 1024)
+        return bail(fail(MCC_EINVAL, "too many edges / Schur pairs of one photo group for k_group's LDS"));
+    HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->use_group ? p->group_shmem : 0));
 #undef HIPC
     (void)rc;
     *out = p;
@@ -1069,7 +1091,7 @@ int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges)
 
 int mcc_problem_path(const mcc_problem* p, int* split_step, int* photo_groups) {
     if (!p) return fail(MCC_EINVAL, "null problem");
-    if (split_step) *split_step = p->fused ? 0 : 1;
+    if (split_step) *split_step = p->fused ? 0 : (p->use_group ? 2 : 1);
     if (photo_groups) *photo_groups = p->fused ? 0 : p->n_pgroups;
     return MCC_OK;
 }

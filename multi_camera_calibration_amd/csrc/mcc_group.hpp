@@ -1,0 +1,762 @@
+// mcc_group.hpp -- the fused split step k_group (included by mcc_kernels.hip, namespace mcc).
+//
+// One 256-thread workgroup per group of consecutive photo vertices (host-built: at most kPhotoGroup
+// photos and kGroupRound edges, or one photo with more edges), doing in ONE launch what k_prep,
+// k_edge and k_photo do in three (src/mymulticalib.cpp:468-614, 668-818; src/multicalib.cpp:593-824;
+// src/doubleSide.cpp:288-581):
+//   phase 0  loads of the group (one round trip: edge records, Schur pair lists, the previous step's
+//            Y', z', dg, the cameras, the first round's corners); the pending photo update
+//            x = fl32(x + fl32(alpha (z' - sum_e Y'_e^T dg))) (k_prep's, group-cooperative), the
+//            cameras' Rodrigues tables (one lane per camera), the photos' Rodrigues (one lane per
+//            photo);
+//   phase A  per round of 16 edges (4 waves x 4 edges x 16 lanes, k_edge's strided lane map): the
+//            edge prologue by the edge's 16 lanes (compose_motion, float32 composed pose, chain maps;
+//            lanes own matrix entries), the corner sweep and the 16-lane butterfly of the 27
+//            normal-equation sums (k_edge's), and the chain H = G^T A' G, g = G^T b' into the group's
+//            LDS -- nothing per edge goes through HBM (k_prep -> k_edge -> k_photo wrote and re-read
+//            erec / echain / eh: 66 + 90 doubles per edge);
+//   phase B  k_photo's per-photo Cholesky, z', U / Y', and the group's Schur pair products written
+//            once per (group, camera-pair block) slot for k_schur.
+// Every reduction keeps the split step's fixed order (edge order within a photo, the pair lists'
+// contribution order), so a run is bitwise reproducible.
+
+// kGroupRound, kGChunk, kGRec and the LDS layout (group_layout) are in mcc_internal.h (host + device).
+
+// The edge prologue by the edge's 16 lanes (sub = 0..15): prep_edge's chain (compose_motion of
+// photo and camera, src/multicalib.cpp:1008-1056, called at src/mymulticalib.cpp:498-500; BACK:
+// compose_motion(ds, photofront), :503-518 / src/doubleSide.cpp:320-328; the float32 composed pose,
+// src/mymulticalib.cpp:546-553; the chain maps), with lanes owning the entries of each 3x3
+// product.  S: 84 doubles of scratch.  Outputs: P[0..11] = R, T of the float32 pose; Gb = the
+// chain maps' nonzero blocks [Gp11, Gp21, Gp22 | pad | Gg11, Gg21, Gg22 | pad].
+template <int MODEL, bool BACK>
+__device__ __forceinline__ void group_prologue(const double* ph, const double* ct, const double* sds, int side,
+                                               int sub, double* S, double* P, double* Gb) {
+    const double* R1 = ph;
+    const double* Jr1 = ph + 9;
+    const double* T1 = ph + 18;
+    const double* R2 = ct;
+    const double* Jl2 = ct + 9;
+    const double* T2 = ct + 18;
+    double* X = S;        // R3 [0..8], T3 [9..11], q [12..14]
+    double* W = S + 15;   // A1 [0..8], A2 [9..17], B2 [18..26]
+    // ---- compose_motion(photo, camera): R3 = R2 R1, q = R2 T1, T3 = q + T2 (OpenCV order)
+    if (sub < 9) {
+        const int i = sub / 3, j = sub % 3;
+        X[sub] = dot3_nc(R2[i * 3], R1[j], R2[i * 3 + 1], R1[3 + j], R2[i * 3 + 2], R1[6 + j]);
+    } else if (sub < 12) {
+        const int i = sub - 9;
+        const double q = dot3_nc(R2[i * 3], T1[0], R2[i * 3 + 1], T1[1], R2[i * 3 + 2], T1[2]);
+        X[12 + i] = q;
+        X[9 + i] = add_nc(q, T2[i]);
+    }
+    wave_sync_lds();
+    double om[3], th, sn, cs;
+    {
+        double R3[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R3[k] = X[k];
+        rodrigues_m2v(R3, om, th, sn, cs);
+    }
+    // ---- A1 = Jr^-1(om3) Jr(om1), A2 = Jl^-1(om3) Jl(om2), B2 = -[q]x Jl(om2)
+    for (int e = sub; e < 27; e += 16) {
+        const int blk = e / 9, ee = e % 9, i = ee / 3, j = ee % 3;
+        double row[3];
+        if (blk < 2) {
+            so3_poly_row(om, blk == 0 ? 0.5 : -0.5, jinv_coef(th, sn, cs), i, row);
+        } else {
+            const double q[3] = {X[12], X[13], X[14]};
+            negskew_row(q, i, row);
+        }
+        const double* B = blk == 0 ? Jr1 : Jl2;
+        W[e] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+    }
+    wave_sync_lds();
+    if (!BACK || side != MCC_BACK) {
+        // float32 composed pose, its Rodrigues (for the projection) and Jl
+        double rf[3], Tf[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)om[k]; Tf[k] = (double)(float)X[9 + k]; }
+        Rot rp;
+        rodrigues_near(rf, th, sn, cs, rp);
+        double ja, jb;
+        jac_coef(rp.th, rp.s, rp.c, ja, jb);
+        if (sub == 0) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) P[k] = rp.R[k];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) P[9 + k] = Tf[k];
+        }
+        // Gp = [[Jl A1, 0], [0, R2]];  Gg = [[Jl A2, 0], [B2, I]] (DoubleSide front: 0,
+        // src/doubleSide.cpp:335-336)
+        for (int t = sub; t < 54; t += 16) {
+            const int w = t / 27, blk = (t % 27) / 9, ee = t % 9, i = ee / 3, j = ee % 3;
+            double v;
+            if (w == 1 && MODEL == MCC_MODEL_DOUBLESIDE) {
+                v = 0.0;
+            } else if (blk == 0) {
+                double row[3];
+                so3_poly_row(rf, ja, jb, i, row);
+                const double* M = w == 0 ? W : W + 9;
+                v = row[0] * M[j] + row[1] * M[3 + j] + row[2] * M[6 + j];
+            } else if (blk == 1) {
+                v = w == 0 ? 0.0 : W[18 + ee];
+            } else {
+                v = w == 0 ? R2[ee] : (i == j ? 1.0 : 0.0);
+            }
+            Gb[28 * w + 9 * blk + ee] = v;
+        }
+        return;
+    }
+    // ---- BACK: compose_motion(ds, photofront); R(om_front) is the FP64 composed rotation R3
+    double fa, fb;
+    jac_coef(th, sn, cs, fa, fb);   // Jlf = Jl(om_front) = I + fa [om]x + fb [om]x^2
+    double* Xb = S + 42;   // Rb [0..8], Tb [9..11], qb [12..14]
+    double* Wb = S + 57;   // A1b [0..8], A2b [9..17], B2b [18..26]
+    const double* Rds = sds;
+    const double* Jrds = sds + 9;
+    const double* dst = sds + 18;
+    if (sub < 9) {
+        const int i = sub / 3, j = sub % 3;
+        Xb[sub] = dot3_nc(X[i * 3], Rds[j], X[i * 3 + 1], Rds[3 + j], X[i * 3 + 2], Rds[6 + j]);
+    } else if (sub < 12) {
+        const int i = sub - 9;
+        const double q = dot3_nc(X[i * 3], dst[0], X[i * 3 + 1], dst[1], X[i * 3 + 2], dst[2]);
+        Xb[12 + i] = q;
+        Xb[9 + i] = add_nc(q, X[9 + i]);
+    }
+    wave_sync_lds();
+    double omb[3], thb, snb, csb;
+    {
+        double Rb[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rb[k] = Xb[k];
+        rodrigues_m2v(Rb, omb, thb, snb, csb);
+    }
+    // A1b = Jr^-1(omb) Jr(ds), A2b = Jl^-1(omb) Jlf, B2b = -[qb]x Jlf
+    {
+        double Jlf[9];
+        so3_poly(om, fa, fb, Jlf);
+        for (int e = sub; e < 27; e += 16) {
+            const int blk = e / 9, ee = e % 9, i = ee / 3, j = ee % 3;
+            double row[3];
+            if (blk < 2) {
+                so3_poly_row(omb, blk == 0 ? 0.5 : -0.5, jinv_coef(thb, snb, csb), i, row);
+            } else {
+                const double q[3] = {Xb[12], Xb[13], Xb[14]};
+                negskew_row(q, i, row);
+            }
+            const double* B = blk == 0 ? Jrds : Jlf;
+            Wb[e] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+        }
+    }
+    wave_sync_lds();
+    double rf[3], Tf[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { rf[k] = (double)(float)omb[k]; Tf[k] = (double)(float)Xb[9 + k]; }
+    Rot rp;
+    rodrigues_near(rf, thb, snb, csb, rp);
+    double ja, jb;
+    jac_coef(rp.th, rp.s, rp.c, ja, jb);
+    if (sub == 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) P[k] = rp.R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) P[9 + k] = Tf[k];
+    }
+    // Gp = [[Jl A2b A1, 0], [B2b A1, R2]] (:509-512); Gg (MyMulti, hazard A12: :514-517 omit
+    // dTt/dTf dTf/dRc) = [[Jl A2b A2, 0], [B2b A2, I]]; Gg (DoubleSide ds, doubleSide.cpp:398-399)
+    // = [[Jl A1b, 0], [0, R_front]]
+    for (int t = sub; t < 54; t += 16) {
+        const int w = t / 27, blk = (t % 27) / 9, ee = t % 9, i = ee / 3, j = ee % 3;
+        const bool ds = w == 1 && MODEL == MCC_MODEL_DOUBLESIDE;
+        const double* M = w == 0 ? W : W + 9;   // A1 (photo) / A2 (camera)
+        double v;
+        if (blk == 0) {
+            double row[3];
+            so3_poly_row(rf, ja, jb, i, row);
+            if (ds) {
+                v = row[0] * Wb[j] + row[1] * Wb[3 + j] + row[2] * Wb[6 + j];
+            } else {
+                double t9[3];   // column j of A2b M
+#pragma unroll
+                for (int k = 0; k < 3; ++k) t9[k] = Wb[9 + k * 3] * M[j] + Wb[9 + k * 3 + 1] * M[3 + j] + Wb[9 + k * 3 + 2] * M[6 + j];
+                v = row[0] * t9[0] + row[1] * t9[1] + row[2] * t9[2];
+            }
+        } else if (blk == 1) {
+            v = ds ? 0.0 : Wb[18 + i * 3] * M[j] + Wb[18 + i * 3 + 1] * M[3 + j] + Wb[18 + i * 3 + 2] * M[6 + j];
+        } else {
+            v = w == 0 ? R2[ee] : (ds ? X[ee] : (i == j ? 1.0 : 0.0));
+        }
+        Gb[28 * w + 9 * blk + ee] = v;
+    }
+}
+
+// The chain of one edge from LDS (k_edge's edge_chain_xh with the chain-map blocks read from Gb
+// and H written into the edge's group record): X_w = A' G_w (X_p with b' as a seventh column),
+// then [Hpp | gp] = Gp^T [Xp | b'], [Hgp | gg] = Gg^T [Xp | b'], Hgg = Gg^T Xg.  Record layout:
+// rec[0..20] Hgg upper, rec[22..57] Hgp (U after k_photo's step), rec[58..63] gg,
+// rec[64..84] Hpp upper, rec[85..90] gp.  Every lane of the wave calls it (wave-level syncs).
+struct GroupChain {
+    double A[36], B[8];
+    double X[2][6][8];
+};
+__device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, int sq, bool valid, double* rec) {
+    if (sq < 12) {
+        const int w = sq / 6, i = sq % 6;
+        double ar[6], gm[28], xr[8];
+        const double2* A2 = reinterpret_cast<const double2*>(CH.A + 6 * i);
+        const double2* G2 = reinterpret_cast<const double2*>(Gbe + 28 * w);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) { const double2 v = A2[q]; ar[2 * q] = v.x; ar[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int q = 0; q < 14; ++q) { const double2 v = G2[q]; gm[2 * q] = v.x; gm[2 * q + 1] = v.y; }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s2 += ar[k] * gm[k * 3 + j];            // G11
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s2 += ar[3 + k] * gm[9 + k * 3 + j];   // G21
+            xr[j] = s2;
+            double s3 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) s3 += ar[3 + k] * gm[18 + k * 3 + j];  // G22
+            xr[3 + j] = s3;
+        }
+        xr[6] = w == 0 ? CH.B[i] : 0.0;
+        xr[7] = 0.0;
+        double2* X2 = reinterpret_cast<double2*>(CH.X[w][i]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X2[q] = make_double2(xr[2 * q], xr[2 * q + 1]);
+    }
+    wave_sync_lds();
+    if (sq < 9 && valid) {
+        const int T = sq / 3, i = sq % 3;
+        const double* Gl = Gbe + 28 * (T == 0 ? 0 : 1);
+        const double2* X2 = reinterpret_cast<const double2*>(CH.X[T == 2 ? 1 : 0][0]);
+        double c11[3], c21[3], c22[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            c11[k] = Gl[k * 3 + i];
+            c21[k] = Gl[9 + k * 3 + i];
+            c22[k] = Gl[18 + k * 3 + i];
+        }
+        double h[7], h2[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) { h[j] = 0.0; h2[j] = 0.0; }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            double xk[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { const double2 v = X2[4 * k + q]; xk[2 * q] = v.x; xk[2 * q + 1] = v.y; }
+            const double c = k < 3 ? c11[k] : c21[k - 3];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) h[j] += c * xk[j];
+            if (k >= 3) {
+#pragma unroll
+                for (int j = 0; j < 7; ++j) h2[j] += c22[k - 3] * xk[j];
+            }
+        }
+        // T = 0: Hpp (upper, rows i, i + 3) and gp; T = 1: Hgp (rows i, i + 3) and gg; T = 2: Hgg
+        const int i2 = i + 3;
+        if (T == 1) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                rec[22 + 6 * i + j] = h[j];
+                rec[22 + 6 * i2 + j] = h2[j];
+            }
+            rec[58 + i] = h[6];
+            rec[58 + i2] = h2[6];
+        } else {
+            double* base = rec + (T == 0 ? 64 : 0);
+            double* o1 = base + 6 * i - i * (i - 1) / 2 - i;
+            double* o2 = base + 6 * i2 - i2 * (i2 - 1) / 2 - i2;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                if (j >= i) o1[j] = h[j];
+                if (j >= i2) o2[j] = h2[j];
+            }
+            if (T == 0) {
+                rec[85 + i] = h[6];
+                rec[85 + i2] = h2[6];
+            }
+        }
+    }
+}
+
+#ifndef MCC_GROUP_OCC
+#define MCC_GROUP_OCC 2   // k_group workgroups per CU the register budget allows (LDS: ~64 KB each)
+#endif
+template <int MODEL, bool RATIONAL, bool PRISM, bool BACK>
+__global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
+    State* st = a.state;
+    const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
+    const int done = st->done, pending = st->pending;
+    const double alpha_prev = st->alpha;   // step factor of the pending update
+    const int p0 = a.pgrp_ptr[grp], np = a.pgrp_ptr[grp + 1] - p0;
+    const int ge0 = a.pgrp_edge[grp], gne = a.pgrp_edge[grp + 1] - ge0;   // the group's edges are contiguous
+    const int q0 = a.gpair_ptr[grp], nq = a.gpair_ptr[grp + 1] - q0;
+    const int c0 = a.gcon_ptr[grp], nc = a.gcon_ptr[grp + 1] - c0;
+    if (done) return;
+    const int C = a.n_cams, m = a.global_dim;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const GroupLayout GL = group_layout(gne, C, nq, nc);
+    double* rec = smem + GL.rec;
+    double* s27 = smem + GL.s27;
+    double* sLi = smem + GL.sLi;
+    double* sv = smem + GL.sv;
+    double* sph = smem + GL.sph;
+    double* sxn = smem + GL.sxn;
+    double* spart = smem + GL.spart;
+    double* sdg = smem + GL.sdg;
+    double* ctab = smem + GL.ctab;
+    double* ktab = smem + GL.ktab;
+    double* sds = smem + GL.sds;
+    double* sP = smem + GL.sP;
+    double* sGb = smem + GL.sGb;
+    int* ibase = reinterpret_cast<int*>(smem + GL.ndoubles);
+    int4* sInfo = reinterpret_cast<int4*>(ibase + GL.iInfo);
+    int* sgb = ibase + GL.iGb;
+    int* seq = ibase + GL.iEq;
+    int* sph0 = ibase + GL.iPh;
+    int4* spq = reinterpret_cast<int4*>(ibase + GL.iPq);
+    unsigned* scn = reinterpret_cast<unsigned*>(ibase + GL.iCn);
+    // this wave's corner staging [5][kGChunk][4] (union with its chain records after the sweep)
+    float(*sC)[kGChunk][4] = reinterpret_cast<float(*)[kGChunk][4]>(smem + GL.sU + wave * (5 * kGChunk * 4 / 2));
+    GroupChain* sCH = reinterpret_cast<GroupChain*>(smem + GL.sU + wave * (5 * kGChunk * 4 / 2));
+    static_assert(4 * sizeof(GroupChain) <= 5 * kGChunk * 4 * sizeof(float), "k_group chain union");
+
+    const int g = lane & 3, sub = lane >> 2;   // edge slot of the wave, lane within the edge
+    // corners of an edge -> this wave's staging (every load of the chunk issued before the first store)
+    auto stage = [&](int eoff, int cc0, int cn) {
+        constexpr int PER = kGChunk / kGroupRound;
+        float v[PER][5];
+        int sb = sub;
+        asm volatile("" : "+v"(sb));
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = sb + kGroupRound * u;
+            const unsigned c = (unsigned)(eoff + cc0 + (i < cn ? i : 0));
+            v[u][0] = a.obj_x[c];
+            v[u][1] = a.obj_y[c];
+            v[u][2] = a.obj_z[c];
+            v[u][3] = a.img_u[c];
+            v[u][4] = a.img_v[c];
+        }
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+            const int i = sb + kGroupRound * u;
+            if (i < cn) {
+#pragma unroll
+                for (int f = 0; f < 5; ++f) sC[f][i][g] = v[u][f];
+            }
+        }
+    };
+
+    // ---- phase 0: every load of the group in one round trip
+    {
+        // the first round's corners (issued first: the longest stream)
+        {
+            const int le = wave * 4 + g;
+            const int4 info = le < gne ? a.edge_info[ge0 + le] : make_int4(0, 0, 0, 0);
+            if (le < gne) stage(info.z, 0, min(info.w, kGChunk));
+        }
+        // edge records, the group's pair lists
+        for (int t = tid; t < gne; t += 256) {
+            sInfo[t] = a.edge_info[ge0 + t];
+            sgb[t] = a.gblock[ge0 + t];
+            seq[t] = a.edge_lphoto[ge0 + t];
+        }
+        if (tid <= np) sph0[tid] = a.photo_ptr[p0 + tid] - ge0;
+        for (int t = tid; t < nq; t += 256) spq[t] = a.gpairs[q0 + t];
+        for (int t = tid; t < nc; t += 256) scn[t] = a.gcon[c0 + t];
+        for (int t = tid; t < m; t += 256) sdg[t] = a.dg[t];
+        if (tid >= 128 && tid < 128 + C) {   // camera tables (k_linearize's wave-1 code)
+            const int c = tid - 128;
+            double om2[3], T2[3];
+            if (MODEL == MCC_MODEL_DOUBLESIDE) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * c + k]; T2[k] = a.cam_rt[6 * c + 3 + k]; }
+            } else if (c == 0) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { om2[k] = 0.0; T2[k] = 0.0; }   // src/mymulticalib.cpp:721-725
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { om2[k] = a.x[6 * (c - 1) + k]; T2[k] = a.x[6 * (c - 1) + 3 + k]; }
+            }
+            double* kt = ktab + 20 * c;
+            const float* Kc = a.K + 9 * c;
+            kt[0] = Kc[0]; kt[1] = Kc[4]; kt[2] = Kc[2]; kt[3] = Kc[5]; kt[4] = Kc[1];
+            kt[5] = MODEL == MCC_MODEL_OMNI ? (double)a.xi[c] : 0.0;
+            const int nd = a.nd;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) kt[6 + q] = q < nd ? (double)a.D[nd * c + q] : 0.0;
+            Rot r2;
+            rodrigues_v2m(om2, r2);
+            double J[9];
+            so3_jac(om2, r2, +1.0, J);
+            double* ct = ctab + 24 * c;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { ct[k] = r2.R[k]; ct[9 + k] = J[k]; }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) ct[18 + k] = T2[k];
+        } else if (BACK && tid == 191) {   // the double-side transform (BACK edges; DoubleSide's global block)
+            double dsr[3];
+            if (MODEL == MCC_MODEL_DOUBLESIDE) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { dsr[k] = a.x[k]; sds[18 + k] = a.x[3 + k]; }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) { dsr[k] = a.ds_rt[k]; sds[18 + k] = a.ds_rt[3 + k]; }
+            }
+            Rot rd;
+            rodrigues_v2m(dsr, rd);
+            double J[9];
+            so3_jac(dsr, rd, -1.0, J);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { sds[k] = rd.R[k]; sds[9 + k] = J[k]; }
+        }
+    }
+    // the pending update's operands: thread (le, k) < 6 gne forms sum_i Y'_e[i][k] dg_g(e)[i]
+    // (k_prep's order); thread 192 + 6q + k < 192 + 6 np: photo q's x_k and z'_k
+    float xo = 0.f;
+    double zk = 0.0;
+    const int pq = (tid - 192) / 6, pk = (tid - 192) % 6;
+    const bool ptask = tid >= 192 && pq < np;
+    if (ptask) {
+        xo = a.x[m + 6 * (size_t)(p0 + pq) + pk];
+        if (pending) zk = a.zp[6 * (size_t)(p0 + pq) + pk];
+    }
+    __syncthreads();
+    if (pending) {
+        for (int t = tid; t < 6 * gne; t += 256) {
+            const int le = t / 6, k = t % 6;
+            const int gbl = sgb[le];
+            const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+            double y[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) y[i] = Ye[6 * i + k];
+            const double* d = sdg + 6 * (gbl < 0 ? 0 : gbl);
+            double sk = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) sk += y[i] * d[i];
+            spart[6 * le + k] = gbl < 0 ? 0.0 : sk;
+        }
+    }
+    __syncthreads();
+    // the photo update x = fl32(x + fl32(alpha (z' - sum_e Y'_e^T dg))) (k_prep's; src/multicalib.cpp:482-501)
+    if (ptask) {
+        float xn = xo;
+        double Gk = 0.0;
+        if (pending) {
+            double t = zk;
+            for (int le = sph0[pq]; le < sph0[pq + 1]; ++le) t -= spart[6 * le + pk];
+            const float G = (float)(alpha_prev * t);   // G = alpha*delta -> CV_32F (:491-496)
+            xn = xo + G;                                // x = x + G (:501)
+            a.x[m + 6 * (size_t)(p0 + pq) + pk] = xn;
+            Gk = (double)G;
+        }
+        sxn[16 * pq + pk] = (double)xn;
+        sxn[16 * pq + 8 + pk] = Gk;
+    }
+    wave_sync_lds();   // the photo tasks are all in wave 3
+    if (ptask && pk == 0) {   // ||G||^2, ||x||^2 partials (stop test); the photo's Rodrigues
+        const double* xs = sxn + 16 * pq;
+        if (pending) {
+            double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                g2 += xs[8 + q] * xs[8 + q];
+                x2 += xs[q] * xs[q];
+            }
+            a.photo_norm[2 * (size_t)(p0 + pq)] = g2;
+            a.photo_norm[2 * (size_t)(p0 + pq) + 1] = x2;
+        }
+        const double om1[3] = {xs[0], xs[1], xs[2]};
+        Rot r1;
+        rodrigues_v2m(om1, r1);
+        double* ph = sph + 24 * pq;
+        so3_jac(om1, r1, -1.0, ph + 9);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) ph[k] = r1.R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ph[18 + k] = xs[3 + k];
+    }
+    __syncthreads();
+
+    // ---- phase A: rounds of 16 edges
+    for (int rb = 0; rb < gne; rb += kGroupRound) {
+        const int es = wave * 4 + g, le = rb + es;
+        const bool ev = le < gne;
+        const int4 info = ev ? sInfo[le] : make_int4(0, 0, 0, 0);
+        const int cam = info.x;
+        double* P = sP + 32 * es;
+        double* Gbe = sGb + 56 * es;
+        if (rb > 0 && ev) stage(info.z, 0, min(info.w, kGChunk));
+        if (ev) {
+            group_prologue<MODEL, BACK>(sph + 24 * seq[le], ctab + 24 * cam, sds, info.y, sub, rec + kGRec * le, P, Gbe);
+            const double* kt = ktab + 20 * cam;
+            P[12 + sub] = kt[sub];
+            if (sub < 2) P[28 + sub] = kt[16 + sub];
+        }
+        wave_sync_lds();
+        // ---- the sweep (k_edge's): FP64 projection + 2 x 6 J' rows, float32 residual, 27 sums
+        double acc[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) acc[q] = 0.0;
+        const int nn = info.w;
+        for (int cc0 = 0;; cc0 += kGChunk) {
+            if (cc0 >= nn) break;
+            const int cn = min(nn - cc0, kGChunk);
+            if (cc0 > 0) {
+                wave_sync_lds();   // the previous chunk is consumed
+                stage(info.z, cc0, cn);
+                wave_sync_lds();
+            }
+#pragma unroll 1
+            for (int i = sub; i < cn; i += kGroupRound) {
+                int po = 0;
+                asm volatile("" : "+v"(po));
+                const double* Pq = P + po;
+                double R[9], T[3], kd[12];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) R[q] = Pq[q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) T[q] = Pq[9 + q];
+#pragma unroll
+                for (int q = 0; q < 12; ++q) kd[q] = Pq[18 + q];
+                const double fx = Pq[12], fy = Pq[13], cx = Pq[14], cy = Pq[15], sk = Pq[16], xi = Pq[17];
+                const double X = sC[0][i][g], Y = sC[1][i][g], Z = sC[2][i][g];
+                const float ou = sC[3][i][g], ov = sC[4][i][g];
+                double Yr[3], D[6];
+                float u, v;
+                if (MODEL == MCC_MODEL_OMNI)
+                    omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
+                else
+                    pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
+                const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
+                if (a.resid) {
+                    const size_t c = (size_t)info.z + cc0 + i;
+                    a.resid[2 * c] = euf;
+                    a.resid[2 * c + 1] = evf;
+                }
+                const double eu = euf, ev2 = evf;
+                double ju[6], jv[6];   // J' rows: [Y x d, d]
+                ju[0] = Yr[1] * D[2] - Yr[2] * D[1];
+                ju[1] = Yr[2] * D[0] - Yr[0] * D[2];
+                ju[2] = Yr[0] * D[1] - Yr[1] * D[0];
+                ju[3] = D[0]; ju[4] = D[1]; ju[5] = D[2];
+                jv[0] = Yr[1] * D[5] - Yr[2] * D[4];
+                jv[1] = Yr[2] * D[3] - Yr[0] * D[5];
+                jv[2] = Yr[0] * D[4] - Yr[1] * D[3];
+                jv[3] = D[3]; jv[4] = D[4]; jv[5] = D[5];
+                int q = 0;
+#pragma unroll
+                for (int r = 0; r < 6; ++r)
+#pragma unroll
+                    for (int s2 = r; s2 < 6; ++s2, ++q) acc[q] = fma(jv[r], jv[s2], fma(ju[r], ju[s2], acc[q]));
+#pragma unroll
+                for (int r = 0; r < 6; ++r) acc[21 + r] = fma(jv[r], ev2, fma(ju[r], eu, acc[21 + r]));
+            }
+        }
+        // ---- butterfly (k_edge's strided reduce-scatter over the edge's 16 lanes), then the chain
+        int tq = lane;
+        asm volatile("" : "+v"(tq));
+        strided_reduce_scatter<kGroupRound>(acc, tq);
+        const int gq = tq & 3, sq = tq >> 2;
+        const int base = strided_rs_base<kGroupRound>(tq);
+        wave_sync_lds();   // the corners are consumed: the chain records overwrite them
+        {
+            GroupChain& CW = sCH[gq];
+#pragma unroll
+            for (int q = 0; q < 32 / kGroupRound; ++q) {
+                const int idx = base + q;
+                if (idx < 21) {
+                    int r, s2;
+                    tri6(idx, r, s2);
+                    CW.A[r * 6 + s2] = acc[q];
+                    CW.A[s2 * 6 + r] = acc[q];
+                } else if (idx < 27) {
+                    CW.B[idx - 21] = acc[q];
+                }
+            }
+        }
+        wave_sync_lds();
+        {
+            const int eq = rb + wave * 4 + gq;
+            group_chain(sCH[gq], sGb + 56 * (wave * 4 + gq), sq, eq < gne, rec + kGRec * (eq < gne ? eq : 0));
+        }
+        wave_sync_lds();   // this wave's chain records are consumed before the next round's corners
+    }
+    __syncthreads();
+
+    // ---- phase B: k_photo's photo work on the group's LDS records
+    constexpr int ES = kGRec;
+    double* sE = rec;
+    // photo q's Hpp / gp column sums in edge order
+    if (tid < 27 * np) {
+        const int q = tid / 27, col27 = tid % 27;
+        double s = 0.0;
+        for (int le = sph0[q]; le < sph0[q + 1]; ++le) s += rec[kGRec * le + 64 + col27];
+        s27[28 * q + col27] = s;
+    }
+    __syncthreads();
+    if (tid < np) {   // one lane per photo: Cholesky Hpp = L L^T, Li = L^-1, v = Li gp, z' = Li^T v
+        const int q = tid, photo = p0 + q;
+        double A[21], gs[6], Lm[6][6], Li[6][6];
+        const double2* S2 = reinterpret_cast<const double2*>(s27 + 28 * q);
+#pragma unroll
+        for (int k = 0; k < 14; ++k) {
+            const double2 w = S2[k];
+            if (2 * k < 21) A[2 * k] = w.x; else gs[2 * k - 21] = w.x;
+            if (2 * k + 1 < 21) A[2 * k + 1] = w.y; else if (2 * k + 1 < 27) gs[2 * k + 1 - 21] = w.y;
+        }
+        bool bad = false;
+        double idg[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double d = A[6 * j - j * (j - 1) / 2];
+#pragma unroll
+            for (int k = 0; k < j; ++k) d -= Lm[j][k] * Lm[j][k];
+            bad |= !(d > 0.0);
+            const double sd = sqrt(d > 0.0 ? d : 1.0);
+            const double is = 1.0 / sd;
+            Lm[j][j] = sd;
+            idg[j] = is;
+#pragma unroll
+            for (int i = j + 1; i < 6; ++i) {
+                double t = A[6 * j - j * (j - 1) / 2 + (i - j)];   // Hpp(j, i) = Hpp(i, j)
+#pragma unroll
+                for (int k = 0; k < j; ++k) t -= Lm[i][k] * Lm[j][k];
+                Lm[i][j] = t * is;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {   // column j of Li: forward substitution of L x = e_j
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                if (i < j) { Li[i][j] = 0.0; continue; }
+                double t = i == j ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = j; k < i; ++k) t -= Lm[i][k] * Li[k][j];
+                Li[i][j] = t * idg[i];
+            }
+        }
+        double vv[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k <= i; ++k) t += Li[i][k] * gs[k];
+            vv[i] = t;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            double t = 0.0;
+#pragma unroll
+            for (int i = j; i < 6; ++i) t += Li[i][j] * vv[i];
+            a.zp[6 * (size_t)photo + j] = t;
+            a.gp_tot[6 * (size_t)photo + j] = gs[j];
+            sv[6 * q + j] = vv[j];
+        }
+        double2* L2 = reinterpret_cast<double2*>(sLi + 36 * q);
+#pragma unroll
+        for (int k = 0; k < 18; ++k) L2[k] = make_double2(Li[(2 * k) / 6][(2 * k) % 6], Li[(2 * k + 1) / 6][(2 * k + 1) % 6]);
+        if (bad) atomicOr(&st->error, 1);
+    }
+    __syncthreads();
+    for (int t = tid; t < 6 * gne; t += 256) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
+        const int le = t / 6, i = t % 6;
+        double h[6], li[36], u[6], y[6];
+        double2* H2 = reinterpret_cast<double2*>(sE + ES * le + 22 + 6 * i);
+        const double2* I2 = reinterpret_cast<const double2*>(sLi + 36 * seq[le]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) { const double2 w = H2[q]; h[2 * q] = w.x; h[2 * q + 1] = w.y; }
+#pragma unroll
+        for (int q = 0; q < 18; ++q) { const double2 w = I2[q]; li[2 * q] = w.x; li[2 * q + 1] = w.y; }
+        const bool gl = sgb[le] >= 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {   // U[i][j] = sum_{k <= j} Hgp[i][k] Li[j][k]
+            double w = 0.0;
+#pragma unroll
+            for (int k = 0; k <= j; ++k) w += h[k] * li[6 * j + k];
+            u[j] = gl ? w : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {   // Y'[i][j] = sum_{k >= j} U[i][k] Li[k][j]
+            double w = 0.0;
+#pragma unroll
+            for (int k = j; k < 6; ++k) w += u[k] * li[6 * k + j];
+            y[j] = w;
+        }
+        double2* G2 = reinterpret_cast<double2*>(a.Y + 36 * (size_t)(ge0 + le) + 6 * i);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            H2[q] = make_double2(u[2 * q], u[2 * q + 1]);
+            G2[q] = make_double2(y[2 * q], y[2 * q + 1]);
+        }
+    }
+    __syncthreads();
+    // the group's Schur pair products per camera-pair block -> its slot (k_photo's pair tasks)
+    int H = 1;
+    while (H < 32 && 6 * nq * 2 * H <= 256) H *= 2;
+    for (int t = tid; t < 6 * nq * H; t += 256) {
+        const int h = t % H, k = t / H / 6, i0 = (t / H) % 6;
+        const int4 pqv = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}
+        const bool diag = (pqv.z & 2) != 0;
+        double acc[6], racc = 0.0, jacc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[j] = 0.0;
+#pragma unroll 1
+        for (int c = pqv.x + h; c < pqv.x + pqv.y; c += H) {
+            const unsigned w = scn[c];
+            const int ea = w & 255, eb = (w >> 8) & 255, q = w >> 17;
+            const bool self = (w >> 16) & 1;
+            const double2* Y2 = reinterpret_cast<const double2*>(sE + ES * ea + 22 + 6 * i0);
+            const double2* B2 = reinterpret_cast<const double2*>(sE + ES * eb + 22);
+            double y[6];
+#pragma unroll
+            for (int qq = 0; qq < 3; ++qq) { const double2 v = Y2[qq]; y[2 * qq] = v.x; y[2 * qq + 1] = v.y; }
+            const double* Hgg = sE + ES * ea;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                double hb[6];
+#pragma unroll
+                for (int qq = 0; qq < 3; ++qq) { const double2 v = B2[3 * j + qq]; hb[2 * qq] = v.x; hb[2 * qq + 1] = v.y; }
+                double d = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * hb[kk];
+                double hv = 0.0;
+                if (self) {
+                    const int rr = i0 < j ? i0 : j, cc = i0 < j ? j : i0;
+                    hv = Hgg[rr * 6 - rr * (rr - 1) / 2 + (cc - rr)];
+                }
+                acc[j] += self ? hv - d : -d;
+            }
+            if (diag && self) {
+                double d = 0.0;
+#pragma unroll
+                for (int kk = 0; kk < 6; ++kk) d += y[kk] * sv[6 * q + kk];
+                const double gg = sE[ES * ea + 58 + i0];
+                racc += gg - d;
+                jacc += gg;
+            }
+        }
+        for (int o = 1; o < H; o <<= 1) {   // the H parts are lanes t - h .. t - h + H - 1 (H | 64)
+#pragma unroll
+            for (int j = 0; j < 6; ++j) acc[j] += __shfl_xor(acc[j], o);
+            racc += __shfl_xor(racc, o);
+            jacc += __shfl_xor(jacc, o);
+        }
+        if (h == 0) {
+            double* out = a.pairprod + (size_t)pqv.w;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) out[i0 * 6 + j] = acc[j];
+            if (diag) {
+                out[36 + i0] = racc;
+                out[42 + i0] = jacc;
+            }
+        }
+    }
+}

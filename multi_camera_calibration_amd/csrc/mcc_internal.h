@@ -106,6 +106,7 @@ struct LinArgs {
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
 constexpr int kPhotoGroup = 8;        // photos per k_photo workgroup, at most
 constexpr int kPhotoGroupEdges = 64;  // edges per k_photo workgroup, at most
+constexpr int kGroupRound = 16;       // edges per k_group round (4 waves x 4 edges x 16 lanes); its groups' cap
 // k_photo's LDS (doubles, then ints): per edge [Hgg upper 21 | pad | U 36 | gg 6] (64), per photo the
 // Hpp / gp sums [28], Hpp's inverse Cholesky factor Li [36] and v [6]; then per edge gblock and
 // photo (ints), the group's pairs (int4) and contributions (unsigned)
@@ -114,6 +115,48 @@ __host__ __device__ inline size_t photo_lds_doubles(int gne) {
 }
 __host__ __device__ inline size_t photo_lds_bytes(int gne, int npairs, int ncon) {
     return photo_lds_doubles(gne) * 8 + 4 * (size_t)((2 * gne + 3) & ~3) + 16 * (size_t)npairs + 4 * (size_t)ncon;
+}
+
+// k_group (mcc_group.hpp): the fused split step's per-group LDS
+constexpr int kGChunk = 96;       // corners of one edge staged in LDS at a time
+constexpr int kGRec = 92;         // doubles per group edge: sE (64: Hgg upper 21 | pad | U 36 | gg 6)
+                                  // + Hpp upper 21 | gp 6 | pad; the edge's prologue scratch meanwhile
+
+// LDS layout of k_group (offsets in doubles; host and device share it)
+struct GroupLayout {
+    int rec, s27, sLi, sv, sph, sxn, spart, sdg, ctab, ktab, sds, sP, sGb, sU, ndoubles;
+    int iInfo, iGb, iEq, iPh, iPq, iCn, nints;   // int offsets after the doubles
+};
+__host__ __device__ inline GroupLayout group_layout(int gne, int C, int nq, int nc) {
+    GroupLayout L;
+    L.rec = 0;
+    L.s27 = L.rec + kGRec * gne;                // [8][28] per-photo Hpp upper 21 | gp 6 sums
+    L.sLi = L.s27 + 28 * kPhotoGroup;           // [8][36] Li = L^-1 (Hpp = L L^T)
+    L.sv = L.sLi + 36 * kPhotoGroup;            // [8][6]  v = Li gp
+    L.sph = L.sv + 6 * kPhotoGroup;             // [8][24] R1 | Jr1 | T1 of the updated photo
+    L.sxn = L.sph + 24 * kPhotoGroup;           // [8][16] x (6) | pad | G (6) | pad
+    L.spart = L.sxn + 16 * kPhotoGroup;         // [gne][6] Y'_e^T dg partials of the photo update
+    L.sdg = L.spart + 6 * gne;                  // [128] the previous solve's global-block delta
+    L.ctab = L.sdg + 128;                       // [C][24] camera R | Jl | T
+    L.ktab = L.ctab + 24 * C;                   // [C][20] fx fy cx cy skew xi k[12]
+    L.sds = L.ktab + 20 * C;                    // [32] double-side transform Rds | Jrds | dst
+    L.sP = L.sds + 32;                          // [16][32] sweep record: R | T | fx fy cx cy skew xi | k[12]
+    L.sGb = L.sP + 32 * kGroupRound;            // [16][56] chain-map blocks [photo 27 | pad | global 27 | pad]
+    L.sU = L.sGb + 56 * kGroupRound;            // per wave: corners [5][96][4] floats | chain {A 36, B 8, X 96} x 4
+    L.ndoubles = L.sU + 4 * (5 * kGChunk * 4 / 2);
+    L.ndoubles = (L.ndoubles + 1) & ~1;         // 16-B aligned int4 area
+    L.iInfo = 0;                                // int4 [gne] {cam, side, corner offset, n}
+    L.iGb = L.iInfo + 4 * gne;                  // [gne] global block
+    L.iEq = L.iGb + gne;                        // [gne] group-local photo
+    L.iPh = L.iEq + gne;                        // [kPhotoGroup + 1] group-relative first edge of each photo
+    L.iPq = (L.iPh + kPhotoGroup + 1 + 3) & ~3; // int4 [nq] pair tasks
+    L.iCn = L.iPq + 4 * nq;                     // [nc] contributions
+    L.nints = L.iCn + nc;
+    return L;
+}
+__host__ __device__ inline size_t group_lds_bytes(int gne, int C, int nq, int nc) {
+    const GroupLayout L = group_layout(gne, C, nq, nc);
+    return (size_t)L.ndoubles * 8 + (size_t)L.nints * 4;
 }
 
 struct SchurArgs {
@@ -168,7 +211,9 @@ struct ErrArgs {
 // launch wrappers (mcc_kernels.hip)
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp);
 size_t mcc_solve_shmem(int m);
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem);
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem);
+hipError_t mcc_launch_group(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t group_shmem,
+                            hipStream_t s);
 hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
                             hipStream_t s);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);

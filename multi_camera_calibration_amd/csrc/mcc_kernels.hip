@@ -2987,6 +2987,8 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
     }
 }
 
+#include "mcc_group.hpp"
+
 }  // namespace mcc
 
 // ---------------------------------------------------------------- launch wrappers
@@ -3059,8 +3061,44 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem) {
+template <int MODEL, bool RATIONAL, bool PRISM, bool BACK>
+static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
+    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK>), dim3(a.n_pgroups), dim3(256), shmem, s, a);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, bool prism, size_t shmem, hipStream_t s) {
+    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
+    if (model == MCC_MODEL_OMNI) return launch_group_t<MCC_MODEL_OMNI, false, false, false>(a, shmem, s);
+    if (model == MCC_MODEL_DOUBLESIDE) {
+        if (rational && prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, true, true>(a, shmem, s);
+        if (rational) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, false, true>(a, shmem, s);
+        if (prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, false, true, true>(a, shmem, s);
+        return launch_group_t<MCC_MODEL_DOUBLESIDE, false, false, true>(a, shmem, s);
+    }
+    if (a.has_back) {
+        if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, true>(a, shmem, s);
+        if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, true>(a, shmem, s);
+        if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, true>(a, shmem, s);
+        return launch_group_t<MCC_MODEL_PINHOLE, false, false, true>(a, shmem, s);
+    }
+    if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, false>(a, shmem, s);
+    if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, false>(a, shmem, s);
+    if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, false>(a, shmem, s);
+    return launch_group_t<MCC_MODEL_PINHOLE, false, false, false>(a, shmem, s);
+}
+
+hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem) {
     hipError_t err = hipSuccess;
+    if (group_shmem > 64 * 1024) {
+#define SETG(M, R, P, B) hipFuncSetAttribute((const void*)&k_group<M, R, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_shmem)
+        for (hipError_t e : {SETG(1, false, false, false), SETG(2, true, true, true), SETG(2, true, false, true),
+                             SETG(2, false, true, true), SETG(2, false, false, true), SETG(0, true, true, true),
+                             SETG(0, true, false, true), SETG(0, false, true, true), SETG(0, false, false, true),
+                             SETG(0, true, true, false), SETG(0, true, false, false), SETG(0, false, true, false),
+                             SETG(0, false, false, false)})
+            if (e != hipSuccess) err = e;
+#undef SETG
+    }
     const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, max_cpp);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)

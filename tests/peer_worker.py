@@ -2,7 +2,7 @@
 peer transport (mcc_peer_*), several ranks on ONE device (RCCL refuses that; the peer transport
 does not need it).  No torch: the inbox handles travel through files (api.file_allgather).
 
-    python tests/peer_worker.py <case> <rank> <world> <rendezvous dir> <out.npz> [steps]
+    python tests/peer_worker.py <case> <rank> <world> <rendezvous dir> <out.npz> [steps] [eps]
 """
 import os
 import sys
@@ -51,7 +51,7 @@ def main():
     ba.peer_init(handles, world, rank)
     mx = ba.allreduce_max(rank + 0.5)
     d, j = ba.compute_jacobian_extrinsic(q.x0)
-    eps = 1e-8 if q.model == rig.DOUBLESIDE else 1e-7   # doubleSide.hpp:105 / mymulticalib.hpp:96
+    eps = float(sys.argv[7]) if len(sys.argv) > 7 else 1e-7   # the TermCriteria eps the test compares at
     x, _, it, ch = ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=eps)
     # throughput of unconditional steps (the bench's loop) over the transport
     ba.set_params(q.x0)

@@ -62,25 +62,34 @@ CASES = {
     "omni_skew": _omni_skew,
     "cams22_m126": lambda: rig.make_config("config3", n_cams=22, n_views=120),   # largest global block, 19 edges/photo
 }
-# the split step (k_prep -> k_edge -> k_photo -> k_schur -> k_solve) runs every m > 30 problem; these
-# force it (MCC_FUSED=0) on the small-m models and distortion variants the fused step otherwise takes
+# the split step runs every m > 30 problem; these force it (MCC_FUSED=0) on the small-m models and
+# distortion variants the fused step otherwise takes.  "_split" takes the split step's default
+# linearisation kernel for the rig (k_group on these small rigs: groups fit the CUs), "_split3"
+# its three-kernel form (k_prep -> k_edge -> k_photo, MCC_GROUP=0; the larger rigs' default)
 SPLIT = ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd8_rational", "nd12_prism"]
 for _n in SPLIT:
     CASES[_n + "_split"] = CASES[_n]
+for _n in ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd12_prism"]:
+    CASES[_n + "_split3"] = CASES[_n]
+CASES["config3_small_split3"] = CASES["config3_small"]
 
 
 def make_adjuster(name, p):
-    if not name.endswith("_split"):
-        return api.BundleAdjuster(p)
-    old = os.environ.get("MCC_FUSED")
-    os.environ["MCC_FUSED"] = "0"
+    env = {}
+    if name.endswith("_split"):
+        env = {"MCC_FUSED": "0"}
+    elif name.endswith("_split3"):
+        env = {"MCC_FUSED": "0", "MCC_GROUP": "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return api.BundleAdjuster(p)
     finally:
-        if old is None:
-            del os.environ["MCC_FUSED"]
-        else:
-            os.environ["MCC_FUSED"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module", params=sorted(CASES))
