@@ -32,6 +32,8 @@
 
 #include <array>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -128,6 +130,24 @@ inline void check(int rc) {
     if (rc != MCC_OK) throw std::runtime_error(std::string("mcc: ") + mcc_last_error());
 }
 
+// isValidPose (src/multicalib.cpp:107-126): 300 < |t| < 3000 (mm), evaluated in float
+inline bool valid_pose(const float t[3]) {
+    const float r = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+    return r < 3000.f && r > 300.f;
+}
+
+// strict-reference mode: the reference's asserts, which its own build keeps on (CMakeLists.txt sets
+// no build type), abort here too instead of this build's defaults (drop the view / run on)
+inline bool strict_reference_env() {
+    const char* s = std::getenv("MCC_STRICT_REFERENCE");
+    return s && std::atoi(s) != 0;
+}
+[[noreturn]] inline void strict_abort(const char* what, const char* where) {
+    std::fprintf(stderr, "mcc strict-reference mode: assertion `%s' failed (%s)\n", what, where);
+    std::fflush(stderr);
+    std::abort();
+}
+
 class MultiCameraCalibration {
 public:
     enum { PINHOLE, OMNIDIRECTIONAL };            // multicalib.hpp:76-79
@@ -180,7 +200,8 @@ public:
     // computeProjectError and paras2vertex; returns the reference's meanReProjError (also kept
     // in _error for writeParameters)
     double optimizeExtrinsics() {
-        std::vector<float> x = buildParas();
+        if (strictReference) return optimizeExtrinsicsChecked();
+        std::vector<float> x = buildParaVector();
         check(mcc_optimize(problem(), _criteria.type, _criteria.maxCount, _criteria.epsilon, x.data(), &_iters,
                            &_change));
         const double error = computeProjectError(x);
@@ -188,6 +209,69 @@ public:
         _error = error;
         return error;
     }
+
+    // optimizeExtrinsics as the reference runs it with its asserts on (strict-reference mode): the
+    // loop of src/multicalib.cpp:462-514 on the host, one linearisation per step through the
+    // virtual seam (computeJacobianExtrinsic, on the GPU), G = fl32(0.95^(k+1) deltaX),
+    // x = fl32(x + G), change = ||G|| / ||x||; before every step the asserts of the linearisation:
+    // every edge's stored transform and every photo pose isValidPose (src/mymulticalib.cpp:706, 714;
+    // src/multicalib.cpp:624, 629; src/doubleSide.cpp:472, 480) and, for pinhole cameras, every
+    // projected corner inside the 1920 x 1080 image (IsvalidImagePoints, src/multicalib.cpp:704-715,
+    // asserted at src/mymulticalib.cpp:568 and src/doubleSide.cpp:378).  A failed assert aborts.
+    double optimizeExtrinsicsChecked() {
+        for (const edge& e : _edgeList) {
+            const float t[3] = {e.transform[3], e.transform[7], e.transform[11]};
+            if (!valid_pose(t)) strict_abort("isValidPose(Tvectran)", "src/mymulticalib.cpp:706");
+        }
+        std::vector<float> x = buildParaVector();
+        double change = 1.0;
+        int iter = 0;
+        for (;; ++iter) {
+            const int ty = _criteria.type;
+            if ((ty == 1 && iter >= _criteria.maxCount) || (ty == 2 && change <= _criteria.epsilon) ||
+                (ty == 3 && (change <= _criteria.epsilon || iter >= _criteria.maxCount)))
+                break;
+            checkIterate(x);
+            std::vector<double> jinv, jte, delta;
+            computeJacobianExtrinsic(x, jinv, jte, delta);
+            const double alpha = std::pow(0.95, (double)iter + 1.0);
+            double g2 = 0.0, x2 = 0.0;
+            for (size_t i = 0; i < x.size(); ++i) {
+                const float G = (float)(alpha * delta[i]);
+                x[i] = x[i] + G;
+                g2 += (double)G * G;
+            }
+            for (float v : x) x2 += (double)v * v;
+            change = std::sqrt(g2) / std::sqrt(x2);
+        }
+        _iters = iter;
+        _change = change;
+        const double error = computeProjectError(x);
+        paras2vertex(x);
+        _error = error;
+        return error;
+    }
+    // the per-step asserts of optimizeExtrinsicsChecked at parameters x
+    void checkIterate(const std::vector<float>& x) {
+        const int C = _nCamera;
+        for (size_t v = C; v < _vertexList.size(); ++v) {
+            const int col = photoParamCol((int)v);
+            if (!valid_pose(&x[col + 3])) strict_abort("isValidPose(TvecPhoto)", "src/mymulticalib.cpp:714");
+        }
+        if (!checksImagePoints()) return;
+        mcc_problem* p = problem();
+        long long corners = 0;
+        check(mcc_problem_stats(p, &corners, nullptr, nullptr, nullptr));
+        std::vector<float> res(2 * (size_t)corners);
+        check(mcc_debug_residuals(p, x.data(), res.data()));   // fl32(obs - proj), reference corner order
+        for (long long c = 0; c < corners; ++c) {
+            const float u = _img[2 * c] - res[2 * c], v = _img[2 * c + 1] - res[2 * c + 1];
+            if (!(u >= 0 && v >= 0)) strict_abort("x >= 0 && y >= 0", "src/multicalib.cpp:711 (IsvalidImagePoints)");
+            if (!(u < 1920 && v < 1080)) strict_abort("x < 1920 && y < 1080", "src/multicalib.cpp:712 (IsvalidImagePoints)");
+        }
+    }
+    // strict-reference mode (opt-in, or MCC_STRICT_REFERENCE=1): abort where the reference asserts
+    bool strictReference = strict_reference_env();
 
     // ---- the sample's driver (libmcc_host.so)
     // loadImages + initialize + optimizeExtrinsics (src/multicalib.cpp:127-133)
@@ -236,7 +320,7 @@ public:
     }
 
     // buildParas (src/multicalib.cpp:422-440): [vertex 1 .. nVertex-1] x (rvec, tvec)
-    virtual std::vector<float> buildParas() {
+    virtual std::vector<float> buildParaVector() {
         std::vector<float> x;
         for (size_t v = 1; v < _vertexList.size(); ++v) {
             float r[3], t[3];
@@ -304,6 +388,11 @@ public:
 
 protected:
     virtual int model() const { return _camType == OMNIDIRECTIONAL ? MCC_MODEL_OMNI : MCC_MODEL_PINHOLE; }
+    // first parameter column of vertex v >= 1 (buildParas' layout)
+    virtual int photoParamCol(int v) const { return 6 * (v - 1); }
+    // the linearisation asserts its projected corners (the pinhole classes, src/mymulticalib.cpp:568;
+    // the base class's omnidir branch has the check commented out, src/multicalib.cpp:779)
+    virtual bool checksImagePoints() const { return false; }
     virtual void extraDesc(mcc_desc&) {}
 
     mcc_problem* problem() {
@@ -413,9 +502,9 @@ protected:
         return true;
     }
 
-public:
 protected:
     int model() const override { return MCC_MODEL_PINHOLE; }
+    bool checksImagePoints() const override { return true; }
     void extraDesc(mcc_desc& d) override {
         bool any = false;
         for (double v : doubleSideTransform) any = any || v != 0.0;
@@ -450,7 +539,7 @@ public:
     std::vector<Pose> camerasPose;      // doubleSide.hpp:123
     Pose doubleSide = eye4();           // the optimised double-side transform (as a pose)
 
-    std::vector<float> buildParas() override {
+    std::vector<float> buildParaVector() override {
         std::vector<float> x(6);
         pose_to_rt(doubleSide, &x[0], &x[3]);
         for (size_t v = _nCamera; v < _vertexList.size(); ++v) {
@@ -470,6 +559,7 @@ public:
     }
 protected:
     int model() const override { return MCC_MODEL_DOUBLESIDE; }
+    int photoParamCol(int v) const override { return 6 * (v - _nCamera + 1); }
     bool keepView(int) const override { return true; }   // storeReaded: every view (:114-118)
     // findTimStamp (:100-112): another camera saw the OTHER side at the same timestamp
     bool sameTimestampMatches(int n, int nOther) const override { return n != nOther; }

@@ -390,7 +390,8 @@ void MyMultiCameraCalibration::loadImages(const std::set<std::string>& outliers)
                 throw std::runtime_error(file + ": too few corners for solvePnP");
             const std::array<float, 3> om{(float)r[0], (float)r[1], (float)r[2]};
             const std::array<float, 3> tv{(float)t[0], (float)t[1], (float)t[2]};
-            if (!is_valid_pose(tv.data())) {   // the reference asserts (a no-op in release builds)
+            if (!is_valid_pose(tv.data())) {   // the reference asserts (src/mymulticalib.cpp:210, :297)
+                if (strictReference) strict_abort("isValidPose(tvec)", "src/mymulticalib.cpp:210 (calcPatternPose)");
                 ++invalidPoseCount;
                 std::cout << "invalid pattern :" << invalidPoseCount << ", " << file << std::endl;
                 continue;

@@ -20,7 +20,7 @@
 // on the GPU.  --cameras N (required), --min-matches K (nMiniMatches, default 20).
 //
 // --init-only stops after loadImages + initialize (no GPU needed).  --dump-problem writes the
-// problem of the last pass (tests/cpp blob format + photo timestamps) with x0 = buildParas(),
+// problem of the last pass (tests/cpp blob format + photo timestamps) with x0 = buildParaVector(),
 // --dump-result the optimised parameters, error, iterations and the outlier files.
 #include <cstdio>
 #include <cstring>
@@ -55,7 +55,7 @@ void wr(std::ofstream& f, const T* p, size_t n) {
     f.write(reinterpret_cast<const char*>(p), (std::streamsize)(n * sizeof(T)));
 }
 
-// the problem as the C ABI sees it (edge order, photo index = vertex - C), x0 = buildParas()
+// the problem as the C ABI sees it (edge order, photo index = vertex - C), x0 = buildParaVector()
 void dump_problem(MultiCameraCalibration& mc, const std::string& path) {
     const int C = mc._nCamera, V = (int)mc._vertexList.size() - C, E = (int)mc._edgeList.size();
     const int nd = (int)mc._distortCoeffs[0].size();
@@ -95,7 +95,7 @@ void dump_problem(MultiCameraCalibration& mc, const std::string& path) {
     if (has_ds) wr(f, my->doubleSideTransform.data(), 16);
     if (dsc)
         for (int c = 0; c < C; ++c) wr(f, dsc->camerasPose[c].data(), 16);
-    const std::vector<float> x0 = mc.buildParas();
+    const std::vector<float> x0 = mc.buildParaVector();
     wr(f, x0.data(), x0.size());
     std::vector<int> ts;
     for (int v = C; v < C + V; ++v) ts.push_back(mc._vertexList[v].timestamp);
@@ -161,7 +161,7 @@ int main(int argc, char** argv) {
                 char b[40];
                 std::snprintf(b, sizeof b, "%.17g", err);
                 r << "error_exact " << b << "\niterations " << multiCalib.iterations() << "\nx";
-                for (float v : multiCalib.buildParas()) {
+                for (float v : multiCalib.buildParaVector()) {
                     std::snprintf(b, sizeof b, " %.9g", v);
                     r << b;
                 }
@@ -214,7 +214,7 @@ int main(int argc, char** argv) {
             r << "error " << std::to_string(err) << "\n";
             std::snprintf(b, sizeof b, "%.17g", err);
             r << "error_exact " << b << "\niterations " << multiCalib.iterations() << "\nx";
-            for (float v : multiCalib.buildParas()) {
+            for (float v : multiCalib.buildParaVector()) {
                 std::snprintf(b, sizeof b, " %.9g", v);
                 r << b;
             }

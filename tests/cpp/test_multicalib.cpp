@@ -82,7 +82,7 @@ static int selftest() {
         for (size_t i = 0; i < x.size(); ++i) x[i] = 0.01f * (float)(i % 6 + 1) * ((i / 6) % 2 ? -1.f : 1.f) + (i % 6 >= 3 ? 0.5f * (float)i : 0.f);
         mc.paras2vertex(x);
         EXPECT(mc._vertexList[0].pose == eye4());                    // camera 0 is the world frame
-        EXPECT(maxdiff(mc.buildParas(), x) < 1e-6);
+        EXPECT(maxdiff(mc.buildParaVector(), x) < 1e-6);
         EXPECT(mc._vertexList[4].pose[3] == x[6 * 3 + 3]);           // photo vertex 4 -> columns 18..23
     }
     {
@@ -91,7 +91,7 @@ static int selftest() {
         std::vector<float> x(6 * 4);
         for (size_t i = 0; i < x.size(); ++i) x[i] = 0.02f * (float)(i % 6) - 0.03f + (i % 6 >= 3 ? 0.25f * (float)i : 0.f);
         ds.paras2vertex(x);
-        EXPECT(maxdiff(ds.buildParas(), x) < 1e-6);
+        EXPECT(maxdiff(ds.buildParaVector(), x) < 1e-6);
         EXPECT(ds.doubleSide[11] == x[5]);                           // ds tvec first
         EXPECT(ds._vertexList[2].pose[3] == x[6 + 3]);               // first photo vertex after ds
     }
@@ -254,10 +254,10 @@ static int run(const char* in, const char* outp) {
     put(o, "pe_edge", ee);
     // the reference's flow: poses -> buildParas -> optimizeExtrinsics -> paras2vertex
     mc->paras2vertex(x0);
-    const auto xb = mc->buildParas();
+    const auto xb = mc->buildParaVector();
     put(o, "x_built", std::vector<double>(xb.begin(), xb.end()));
     const double err = mc->optimizeExtrinsics();
-    const auto xo = mc->buildParas();
+    const auto xo = mc->buildParaVector();
     put(o, "opt_error", {err});
     put(o, "opt_iters", {(double)mc->iterations()});
     put(o, "opt_change", {mc->lastChange()});

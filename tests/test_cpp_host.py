@@ -119,3 +119,52 @@ def test_cpp_host_golden(exe, tmp_path, path):
     # minimises the squared residuals, not the reported mean L2 error, so the latter may move
     # by a few 1e-5 px)
     assert abs(o["opt2_error"][0] - o["opt_error"][0]) <= 1e-5 * (1.0 + o["opt_error"][0])
+
+
+# ---------------------------------------------------------------- the reference's cv::Mat-typed seam
+SEAM_SRC = os.path.join(ROOT, "tests", "cpp", "test_seam.cpp")
+
+
+@pytest.fixture(scope="module")
+def seam_exe(tmp_path_factory):
+    """tests/cpp/test_seam.cpp: subclasses written the way the reference writes MyMulti /
+    DoubleSide (overriding computeJacobianExtrinsic(const Mat&, Mat&, Mat&, Mat&) etc., mymulticalib.hpp:
+    164-172, doubleSide.hpp:133-165), compiled against include/opencv2/ccalib/*.hpp -- the build
+    itself is the first check."""
+    api.build()
+    libdir = os.path.dirname(api.LIB_PATH)
+    out = str(tmp_path_factory.mktemp("seam") / "test_seam")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "include", "opencv2", "ccalib"), SEAM_SRC, "-L", libdir, "-lmcc_host",
+                    "-lmcc", f"-Wl,-rpath,{libdir}", "-o", out], check=True)
+    return out
+
+
+def test_seam_selftest(seam_exe):
+    """Host only: the cv::Mat shim, the public conjungate (multicalib.hpp:157), compose_motion's
+    partials against central differences, the per-edge CPU Jacobian's loud default."""
+    r = subprocess.run([seam_exe, "selftest"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "selftest ok" in r.stdout
+
+
+def test_seam_strict_reference_aborts(seam_exe):
+    """Strict-reference mode aborts where the reference's assert does (src/mymulticalib.cpp:706:
+    an edge's stored transform failing isValidPose) -- before any device work."""
+    r = subprocess.run([seam_exe, "strict"], capture_output=True, text=True, timeout=60)
+    assert r.returncode in (-6, 134), (r.returncode, r.stdout, r.stderr)
+    assert "isValidPose(Tvectran)" in r.stderr and "src/mymulticalib.cpp:706" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda f: os.path.splitext(os.path.basename(f))[0])
+def test_seam_subclass_runs_reference_loop(seam_exe, tmp_path, path):
+    """A subclass overriding the seam runs the reference's host loop (src/multicalib.cpp:462-514)
+    through its overrides -- computeJacobianExtrinsic once per step, buildParas /
+    computeProjectError / paras2vertex once -- and reaches the library class's device loop: the
+    same iterations, error within 1e-6 px, parameters within 1 ulp."""
+    gd = dict(np.load(path))
+    _write_blob(str(tmp_path / "in.bin"), gd)
+    r = subprocess.run([seam_exe, "run", str(tmp_path / "in.bin")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "seam ok" in r.stdout

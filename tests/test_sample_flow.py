@@ -127,6 +127,29 @@ def test_sample_load_initialize_cpu(sample, tmp_path):
         assert np.abs(xq[3:] - xt[3:]).max() < 20.0
 
 
+def test_strict_reference_invalid_pose(sample, tmp_path):
+    """A view whose solvePnP pose fails isValidPose (300 < |t| < 3000 mm): the default loader drops
+    it with the reference's message (src/mymulticalib.cpp:292-299); strict-reference mode
+    (MCC_STRICT_REFERENCE=1) aborts as the reference's assert does (src/mymulticalib.cpp:210,
+    calcPatternPose).  Host only: the loader runs before any device work."""
+    p = _rig()
+    serials, data, config, files, stamps = SD.write_dataset(p, str(tmp_path))
+    far = sorted(files)[0]   # objects x 4 with the same corners: the same view seen 4x farther away
+    txt = open(far).read()
+    head, objs = txt.split("objects:")
+    e = files[far]
+    o, n = int(p.edge_off[e]), int(p.edge_n[e])
+    with open(far, "w") as f:
+        f.write(head + SD._mat_yaml("objects", 4.0 * np.asarray(p.obj[o:o + n], np.float64)))
+    args = ["--serials", ",".join(serials), "--data", data, "--config", config, "--init-only"]
+    out = _run(sample, args)
+    assert "invalid pattern" in out and far in out
+    r = subprocess.run([sample] + args, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MCC_STRICT_REFERENCE="1"))
+    assert r.returncode in (-6, 134), (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "isValidPose(tvec)" in r.stderr and "src/mymulticalib.cpp:210" in r.stderr
+
+
 def _xml_mat(root, key):
     e = root.find(key)
     rows, cols = int(e.find("rows").text), int(e.find("cols").text)
