@@ -586,7 +586,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // k_group (two workgroups per CU) wins while its groups fit the CUs in one wave of workgroups
     // (config4: 32.3 vs 36.9 us per step); with more groups the three-kernel form's higher
     // occupancy wins (config5: 67.3 vs 61.0, config3: 185.5 vs 120.5).  MCC_GROUP=1 / 0 forces.
-    std::vector<int> pgrp_ptr = make_groups(mcc::kGroupRound);
+    int group_cap = mcc::kGroupRound;   // MCC_GROUP_EDGES: k_group's groups smaller than a round (A/B)
+    if (const char* f = std::getenv("MCC_GROUP_EDGES")) group_cap = std::max(1, std::min(mcc::kGroupRound, std::atoi(f)));
+    std::vector<int> pgrp_ptr = make_groups(group_cap);
     p->use_group = !p->fused && (int)pgrp_ptr.size() - 1 <= n_cu;
     if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
     if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);

@@ -299,6 +299,8 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
     const int q0 = a.gpair_ptr[grp], nq = a.gpair_ptr[grp + 1] - q0;
     const int c0 = a.gcon_ptr[grp], nc = a.gcon_ptr[grp + 1] - c0;
     if (done) return;
+    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)grp : nullptr;   // MCC_DIAG: slots 0..11
+    SSTAMP(stp, 0, 0);
     const int C = a.n_cams, m = a.global_dim;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const GroupLayout GL = group_layout(gne, C, nq, nc);
@@ -419,7 +421,8 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
     }
     // the pending update's operands: thread (le, k) < 6 gne forms sum_i Y'_e[i][k] dg_g(e)[i]
-    // (k_prep's order); thread 192 + 6q + k < 192 + 6 np: photo q's x_k and z'_k
+    // (k_prep's order; its first task's Y' column and global block loaded in this round trip);
+    // thread 192 + 6q + k < 192 + 6 np: photo q's x_k and z'_k
     float xo = 0.f;
     double zk = 0.0;
     const int pq = (tid - 192) / 6, pk = (tid - 192) % 6;
@@ -428,15 +431,31 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         xo = a.x[m + 6 * (size_t)(p0 + pq) + pk];
         if (pending) zk = a.zp[6 * (size_t)(p0 + pq) + pk];
     }
+    double y0[6];
+    int gb0 = -1;
+    if (pending && tid < 6 * gne) {
+        const int le = tid / 6, k = tid % 6;
+        gb0 = a.gblock[ge0 + le];
+        const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) y0[i] = Ye[6 * i + k];
+    }
     __syncthreads();
+    SSTAMP(stp, 1, 0);
     if (pending) {
         for (int t = tid; t < 6 * gne; t += 256) {
             const int le = t / 6, k = t % 6;
-            const int gbl = sgb[le];
-            const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+            int gbl = gb0;
             double y[6];
+            if (t == tid) {
 #pragma unroll
-            for (int i = 0; i < 6; ++i) y[i] = Ye[6 * i + k];
+                for (int i = 0; i < 6; ++i) y[i] = y0[i];
+            } else {
+                gbl = sgb[le];
+                const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y[i] = Ye[6 * i + k];
+            }
             const double* d = sdg + 6 * (gbl < 0 ? 0 : gbl);
             double sk = 0.0;
 #pragma unroll
@@ -484,6 +503,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         for (int k = 0; k < 3; ++k) ph[18 + k] = xs[3 + k];
     }
     __syncthreads();
+    SSTAMP(stp, 2, 0);
 
     // ---- phase A: rounds of 16 edges
     for (int rb = 0; rb < gne; rb += kGroupRound) {
@@ -501,6 +521,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
             if (sub < 2) P[28 + sub] = kt[16 + sub];
         }
         wave_sync_lds();
+        if (rb == 0) SSTAMP(stp, 3, 0);
         // ---- the sweep (k_edge's): FP64 projection + 2 x 6 J' rows, float32 residual, 27 sums
         double acc[32];
 #pragma unroll
@@ -561,6 +582,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
             }
         }
         // ---- butterfly (k_edge's strided reduce-scatter over the edge's 16 lanes), then the chain
+        if (rb == 0) SSTAMP(stp, 4, 0);
         int tq = lane;
         asm volatile("" : "+v"(tq));
         strided_reduce_scatter<kGroupRound>(acc, tq);
@@ -588,8 +610,10 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
             group_chain(sCH[gq], sGb + 56 * (wave * 4 + gq), sq, eq < gne, rec + kGRec * (eq < gne ? eq : 0));
         }
         wave_sync_lds();   // this wave's chain records are consumed before the next round's corners
+        if (rb == 0) SSTAMP(stp, 5, 0);
     }
     __syncthreads();
+    SSTAMP(stp, 6, 0);
 
     // ---- phase B: k_photo's photo work on the group's LDS records
     constexpr int ES = kGRec;
@@ -602,6 +626,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         s27[28 * q + col27] = s;
     }
     __syncthreads();
+    SSTAMP(stp, 7, 0);
     if (tid < np) {   // one lane per photo: Cholesky Hpp = L L^T, Li = L^-1, v = Li gp, z' = Li^T v
         const int q = tid, photo = p0 + q;
         double A[21], gs[6], Lm[6][6], Li[6][6];
@@ -666,6 +691,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         if (bad) atomicOr(&st->error, 1);
     }
     __syncthreads();
+    SSTAMP(stp, 8, 0);
     for (int t = tid; t < 6 * gne; t += 256) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
         const int le = t / 6, i = t % 6;
         double h[6], li[36], u[6], y[6];
@@ -698,6 +724,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
     }
     __syncthreads();
+    SSTAMP(stp, 9, 0);
     // the group's Schur pair products per camera-pair block -> its slot (k_photo's pair tasks)
     int H = 1;
     while (H < 32 && 6 * nq * 2 * H <= 256) H *= 2;
@@ -759,4 +786,9 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
             }
         }
     }
+#ifdef MCC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    SSTAMP(stp, 10, 0);
+#endif
 }

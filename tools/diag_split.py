@@ -4,7 +4,9 @@ diagnostic build (libmcc_diag.so).  Never quote this build's run time: read its 
 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_split.py [config] [views]
 
-Rows of the stamp buffer (32 slots each): k_photo photo p -> row p slots 0..5 (start, staged,
+k_group (the split step's group kernel) group g -> row g slots 0..10 (start, loads, photo update and
+Rodrigues, round 0's prologue, sweep, chain, the later rounds, Hpp sums, Cholesky, U / Y', pairs).
+Otherwise rows of the stamp buffer (32 slots each): k_photo photo p -> row p slots 0..5 (start, staged,
 Cholesky, U / Y', pairs stored; slot 2 unused); k_prep workgroup w -> row w slots 8..11 (start, update,
 photo Rodrigues, edges stored); k_edge workgroup w -> row w / 2 slots 16 + 8 (w & 1) + 0..4
 (start, corners staged, sweep, butterfly, H stored).
@@ -48,6 +50,12 @@ def main():
             print(f"  {n:22s} {med(d[:, k])}")
         print(f"  {'total':22s} {med(blk[ok][:, -1] - blk[ok][:, 0])}")
 
+    if ba.step_kernels() == "k_group":
+        ng = int(np.count_nonzero(s[:, 0]))
+        phases(list(range(11)), ["loads (round trip 1)", "photo update+Rodrigues", "edge prologue (r0)", "sweep (r0)",
+                                 "butterfly+chain (r0)", "later rounds", "photo Hpp sums", "Cholesky", "U, Y'",
+                                 "pairs+store"], f"k_group ({ng} groups)")
+        return
     phases([0, 1, 3, 4, 5], ["load+stage+sums", "Cholesky, Li", "U, Y'", "pairs+store"], "k_photo")
     phases([8, 9, 10, 11], ["photo update", "photo Rodrigues", "edge prologues"], "k_prep")
     for h in (0, 1):

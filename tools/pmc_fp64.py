@@ -42,9 +42,9 @@ def main():
         e["fp64_flops"] = 64.0 * (e.get("SQ_INSTS_VALU_FLOPS_FP64", 0.0) + e.get("SQ_INSTS_VALU_FLOPS_FP64_TRANS", 0.0))
     for e in kernels.values():
         e["fp64_flops_per_corner"] = e["fp64_flops"] / a.corners if a.corners else None
-    step_kernels = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
+    step_kernels = [k for k in ("k_linearize", "k_group", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
     step = sum(kernels[k]["fp64_flops"] for k in step_kernels)
-    lin_k = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo") if k in kernels]
+    lin_k = [k for k in ("k_linearize", "k_group", "k_prep", "k_edge", "k_photo") if k in kernels]
     lin = {"fp64_flops": sum(kernels[k]["fp64_flops"] for k in lin_k)} if lin_k else {}
     out = {"config": a.config, "n_views": a.views, "kernel": "+".join(lin_k),
            "step_kernels": step_kernels, "step_fp64_flops": step,

@@ -37,7 +37,7 @@ def read_counters(d):
 
 
 def short(name):
-    for k in ("k_linearize", "k_schur", "k_solve", "k_backsub", "k_project_error", "k_prep", "k_edge", "k_photo"):
+    for k in ("k_linearize", "k_group", "k_schur", "k_solve", "k_backsub", "k_project_error", "k_prep", "k_edge", "k_photo"):
         if k in name:
             return k
     return name
@@ -71,9 +71,9 @@ def main():
         e["read_bytes_corrected"] = fb
         e["write_bytes"] = wb
         e["bytes_per_launch"] = fb + wb
-    step_kernels = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
+    step_kernels = [k for k in ("k_linearize", "k_group", "k_prep", "k_edge", "k_photo", "k_schur", "k_solve") if k in kernels]
     step_bytes = sum(kernels[k]["bytes_per_launch"] for k in step_kernels)
-    lin_k = [k for k in ("k_linearize", "k_prep", "k_edge", "k_photo") if k in kernels]
+    lin_k = [k for k in ("k_linearize", "k_group", "k_prep", "k_edge", "k_photo") if k in kernels]
     lin = {"bytes_per_launch": sum(kernels[k]["bytes_per_launch"] for k in lin_k)} if lin_k else {}
     out = {
         "config": a.config, "n_views": a.views, "kernel": "+".join(lin_k),
