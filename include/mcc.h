@@ -159,6 +159,12 @@ int mcc_peer_enable(mcc_problem *p, int on);
 /* ---- diagnostics / measurement */
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
+/* test / measurement: the m > 30 dense solve alone (k_solve's elimination), x = S^-1 r for a
+ * packed SPD system [S upper triangle row-major, m(m+1)/2 | r, m] on `device`; with reps > 0 the
+ * average device time of `reps` back-to-back launches (one workgroup each) in *us_per_solve; with
+ * stamps (64 entries) the elimination's per-phase s_memtime stamps of the first launch. */
+int mcc_debug_solve(int device, int m, const double *packed, double *x, int reps, double *us_per_solve,
+                    long long *stamps);
 /* average device time (ms) per launch of the linearisation kernel over the last
  * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches.
  * Fused single-GPU problems (m <= 30 and at most two photos per CU: one kernel per step) time

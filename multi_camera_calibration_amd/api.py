@@ -119,6 +119,8 @@ def lib():
         L.mcc_comm_barrier.argtypes = [ctypes.c_void_p]
         L.mcc_partition_photos.argtypes = [ctypes.c_int, ctypes.c_int, _i32p, _i32p, ctypes.c_int, _i32p]
         L.mcc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+        L.mcc_debug_solve.argtypes = [ctypes.c_int, ctypes.c_int, _f64p, _f64p, ctypes.c_int, _f64p,
+                                      ctypes.POINTER(ctypes.c_longlong)]
         L.mcc_peer_handle.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.mcc_peer_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
         L.mcc_peer_enable.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -139,6 +141,23 @@ def lib():
                                             _f64p, _f64p, _f64p, _f64p, _f64p, _i32p, _i32p, _f64p, _i32p]
         _LIB = L
     return _LIB
+
+
+def debug_solve(S, r, reps=0, stamps=False, device=0):
+    """k_solve's m > 30 elimination alone on the SPD system S x = r (mcc_debug_solve): returns x,
+    the average device microseconds per solve over `reps` launches (None without reps) and, with
+    stamps, the first launch's 64 per-phase s_memtime stamps."""
+    S = np.asarray(S, np.float64)
+    m = S.shape[0]
+    iu = np.triu_indices(m)
+    packed = np.ascontiguousarray(np.concatenate([S[iu], np.asarray(r, np.float64)]))
+    x = np.zeros(m, np.float64)
+    us = np.zeros(1, np.float64)
+    st = np.zeros(64, np.int64)
+    _check(lib().mcc_debug_solve(device, m, _ptr(packed, _f64p), _ptr(x, _f64p), int(reps), _ptr(us, _f64p),
+                                 st.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)) if stamps else None),
+           "mcc_debug_solve")
+    return x, (float(us[0]) if reps else None), (st if stamps else None)
 
 
 def declared_symbols():

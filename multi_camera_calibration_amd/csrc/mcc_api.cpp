@@ -146,6 +146,7 @@ struct mcc_problem {
     // photo Schur work) instead of k_prep -> k_edge -> k_photo; MCC_GROUP=0 selects the three
     int use_group = 1;
     size_t group_shmem = 0;
+    int group_lanes = 32;   // k_group's lanes per edge (32: 512-thread workgroups; 16: 256)
     // fused single-kernel step (m <= kFusedMaxM): photo contributions + two-level reduction
     static constexpr int kFusedMaxM = 30;
     int fused = 0, group_size = 1, n_groups = 1;
@@ -277,7 +278,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.erec = p->erec.p; la.echain = p->echain.p; la.eh = p->eh.p;
     if (p->V > 0) {
         if (!p->fused && p->use_group)
-            HIPCHK(mcc_launch_group(la, p->model, p->rational, p->prism, p->group_shmem, p->stream));
+            HIPCHK(mcc_launch_group(la, p->model, p->rational, p->prism, p->group_lanes, p->group_shmem, p->stream));
         else if (!p->fused)
             HIPCHK(mcc_launch_split(la, p->model, p->rational, p->prism, p->photo_shmem, p->stream));
         else
@@ -592,6 +593,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->use_group = !p->fused && (int)pgrp_ptr.size() - 1 <= n_cu;
     if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
     if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);
+    if (const char* f = std::getenv("MCC_GROUP_LANES")) p->group_lanes = std::atoi(f) == 16 ? 16 : 32;
     const int NG = (int)pgrp_ptr.size() - 1;
     std::vector<int4> gpairs;                           // {first contribution, count, diagonal << 1, slot}
     std::vector<unsigned> gcon;
@@ -961,6 +963,53 @@ int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* m
     }
     if (mean) *mean = npts ? (double)total / (double)npts : 0.0;
     return MCC_OK;
+}
+
+int mcc_debug_solve(int device, int m, const double* packed, double* x, int reps, double* us_per_solve,
+                    long long* stamps) {
+    if (m <= 30 || m > 128 || !packed || !x) return fail(MCC_EINVAL, "mcc_debug_solve: 30 < m <= 128, non-null buffers");
+    HIPCHK(hipSetDevice(device));
+    const size_t n = (size_t)m * (m + 1) / 2 + (size_t)m;
+    struct Bufs {
+        double* pk = nullptr;
+        double* xd = nullptr;
+        int* err = nullptr;
+        long long* st = nullptr;
+        hipStream_t s = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Bufs() {
+            (void)hipFree(pk); (void)hipFree(xd); (void)hipFree(err); (void)hipFree(st);
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } b;
+    HIPCHK(hipMalloc(&b.pk, n * sizeof(double)));
+    HIPCHK(hipMalloc(&b.xd, (size_t)m * sizeof(double)));
+    HIPCHK(hipMalloc(&b.err, sizeof(int)));
+    HIPCHK(hipMalloc(&b.st, 64 * sizeof(long long)));
+    HIPCHK(hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking));
+    HIPCHK(hipMemcpy(b.pk, packed, n * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(b.err, 0, sizeof(int)));
+    HIPCHK(hipMemset(b.st, 0, 64 * sizeof(long long)));
+    HIPCHK(mcc_launch_debug_solve(b.pk, b.xd, m, b.err, stamps ? b.st : nullptr, b.s));
+    HIPCHK(hipStreamSynchronize(b.s));
+    int err = 0;
+    HIPCHK(hipMemcpy(x, b.xd, (size_t)m * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&err, b.err, sizeof(int), hipMemcpyDeviceToHost));
+    if (stamps) HIPCHK(hipMemcpy(stamps, b.st, 64 * sizeof(long long), hipMemcpyDeviceToHost));
+    if (reps > 0 && us_per_solve) {
+        HIPCHK(hipEventCreate(&b.e0));
+        HIPCHK(hipEventCreate(&b.e1));
+        HIPCHK(hipEventRecord(b.e0, b.s));
+        for (int r = 0; r < reps; ++r) HIPCHK(mcc_launch_debug_solve(b.pk, b.xd, m, b.err, nullptr, b.s));
+        HIPCHK(hipEventRecord(b.e1, b.s));
+        HIPCHK(hipEventSynchronize(b.e1));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, b.e0, b.e1));
+        *us_per_solve = 1e3 * (double)ms / reps;
+    }
+    return err ? fail(MCC_ENOTPD, "mcc_debug_solve: not positive definite") : MCC_OK;
 }
 
 int mcc_debug_residuals(mcc_problem* p, const float* x, float* res) {

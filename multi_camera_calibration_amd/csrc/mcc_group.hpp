@@ -28,7 +28,7 @@
 // src/mymulticalib.cpp:546-553; the chain maps), with lanes owning the entries of each 3x3
 // product.  S: 84 doubles of scratch.  Outputs: P[0..11] = R, T of the float32 pose; Gb = the
 // chain maps' nonzero blocks [Gp11, Gp21, Gp22 | pad | Gg11, Gg21, Gg22 | pad].
-template <int MODEL, bool BACK>
+template <int MODEL, bool BACK, int L>
 __device__ __forceinline__ void group_prologue(const double* ph, const double* ct, const double* sds, int side,
                                                int sub, double* S, double* P, double* Gb) {
     const double* R1 = ph;
@@ -58,7 +58,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         rodrigues_m2v(R3, om, th, sn, cs);
     }
     // ---- A1 = Jr^-1(om3) Jr(om1), A2 = Jl^-1(om3) Jl(om2), B2 = -[q]x Jl(om2)
-    for (int e = sub; e < 27; e += 16) {
+    for (int e = sub; e < 27; e += L) {
         const int blk = e / 9, ee = e % 9, i = ee / 3, j = ee % 3;
         double row[3];
         if (blk < 2) {
@@ -88,7 +88,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         }
         // Gp = [[Jl A1, 0], [0, R2]];  Gg = [[Jl A2, 0], [B2, I]] (DoubleSide front: 0,
         // src/doubleSide.cpp:335-336)
-        for (int t = sub; t < 54; t += 16) {
+        for (int t = sub; t < 54; t += L) {
             const int w = t / 27, blk = (t % 27) / 9, ee = t % 9, i = ee / 3, j = ee % 3;
             double v;
             if (w == 1 && MODEL == MCC_MODEL_DOUBLESIDE) {
@@ -133,21 +133,21 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         rodrigues_m2v(Rb, omb, thb, snb, csb);
     }
     // A1b = Jr^-1(omb) Jr(ds), A2b = Jl^-1(omb) Jlf, B2b = -[qb]x Jlf
-    {
-        double Jlf[9];
-        so3_poly(om, fa, fb, Jlf);
-        for (int e = sub; e < 27; e += 16) {
-            const int blk = e / 9, ee = e % 9, i = ee / 3, j = ee % 3;
-            double row[3];
-            if (blk < 2) {
-                so3_poly_row(omb, blk == 0 ? 0.5 : -0.5, jinv_coef(thb, snb, csb), i, row);
-            } else {
-                const double q[3] = {Xb[12], Xb[13], Xb[14]};
-                negskew_row(q, i, row);
-            }
-            const double* B = blk == 0 ? Jrds : Jlf;
-            Wb[e] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+    for (int e = sub; e < 27; e += L) {
+        const int blk = e / 9, ee = e % 9, i = ee / 3, j = ee % 3;
+        double row[3], bc[3];
+        if (blk < 2) {
+            so3_poly_row(omb, blk == 0 ? 0.5 : -0.5, jinv_coef(thb, snb, csb), i, row);
+        } else {
+            const double q[3] = {Xb[12], Xb[13], Xb[14]};
+            negskew_row(q, i, row);
         }
+        if (blk == 0) {
+            bc[0] = Jrds[j]; bc[1] = Jrds[3 + j]; bc[2] = Jrds[6 + j];
+        } else {
+            so3_poly_col(om, fa, fb, j, bc);   // column j of Jlf (registers: no private array)
+        }
+        Wb[e] = row[0] * bc[0] + row[1] * bc[1] + row[2] * bc[2];
     }
     wave_sync_lds();
     double rf[3], Tf[3];
@@ -166,7 +166,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
     // Gp = [[Jl A2b A1, 0], [B2b A1, R2]] (:509-512); Gg (MyMulti, hazard A12: :514-517 omit
     // dTt/dTf dTf/dRc) = [[Jl A2b A2, 0], [B2b A2, I]]; Gg (DoubleSide ds, doubleSide.cpp:398-399)
     // = [[Jl A1b, 0], [0, R_front]]
-    for (int t = sub; t < 54; t += 16) {
+    for (int t = sub; t < 54; t += L) {
         const int w = t / 27, blk = (t % 27) / 9, ee = t % 9, i = ee / 3, j = ee % 3;
         const bool ds = w == 1 && MODEL == MCC_MODEL_DOUBLESIDE;
         const double* M = w == 0 ? W : W + 9;   // A1 (photo) / A2 (camera)
@@ -287,8 +287,10 @@ __device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, i
 #ifndef MCC_GROUP_OCC
 #define MCC_GROUP_OCC 2   // k_group workgroups per CU the register budget allows (LDS: ~64 KB each)
 #endif
-template <int MODEL, bool RATIONAL, bool PRISM, bool BACK>
-__global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
+template <int MODEL, bool RATIONAL, bool PRISM, bool BACK, int L>
+__global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_group(LinArgs a) {
+    constexpr int NT = kGroupRound * L, EPW = 64 / L;   // threads; edges per wave
+    static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
@@ -325,20 +327,20 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
     int4* spq = reinterpret_cast<int4*>(ibase + GL.iPq);
     unsigned* scn = reinterpret_cast<unsigned*>(ibase + GL.iCn);
     // this wave's corner staging [5][kGChunk][4] (union with its chain records after the sweep)
-    float(*sC)[kGChunk][4] = reinterpret_cast<float(*)[kGChunk][4]>(smem + GL.sU + wave * (5 * kGChunk * 4 / 2));
-    GroupChain* sCH = reinterpret_cast<GroupChain*>(smem + GL.sU + wave * (5 * kGChunk * 4 / 2));
-    static_assert(4 * sizeof(GroupChain) <= 5 * kGChunk * 4 * sizeof(float), "k_group chain union");
+    float(*sC)[kGChunk][EPW] = reinterpret_cast<float(*)[kGChunk][EPW]>(smem + GL.sU + wave * (5 * kGChunk * EPW / 2));
+    GroupChain* sCH = reinterpret_cast<GroupChain*>(smem + GL.sU + wave * (5 * kGChunk * EPW / 2));
+    static_assert(EPW * sizeof(GroupChain) <= 5 * kGChunk * EPW * sizeof(float), "k_group chain union");
 
-    const int g = lane & 3, sub = lane >> 2;   // edge slot of the wave, lane within the edge
+    const int g = lane % EPW, sub = lane / EPW;   // edge slot of the wave, lane within the edge
     // corners of an edge -> this wave's staging (every load of the chunk issued before the first store)
     auto stage = [&](int eoff, int cc0, int cn) {
-        constexpr int PER = kGChunk / kGroupRound;
+        constexpr int PER = kGChunk / L;
         float v[PER][5];
         int sb = sub;
         asm volatile("" : "+v"(sb));
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int i = sb + kGroupRound * u;
+            const int i = sb + L * u;
             const unsigned c = (unsigned)(eoff + cc0 + (i < cn ? i : 0));
             v[u][0] = a.obj_x[c];
             v[u][1] = a.obj_y[c];
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
-            const int i = sb + kGroupRound * u;
+            const int i = sb + L * u;
             if (i < cn) {
 #pragma unroll
                 for (int f = 0; f < 5; ++f) sC[f][i][g] = v[u][f];
@@ -356,27 +358,30 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
     };
 
+    // the cameras' (and the double-side transform's) Rodrigues tables are formed by threads outside
+    // the photo tasks' wave while those update the photos (k_linearize's wave-1 code)
+    constexpr int CAM0 = NT / 2, DST = CAM0 + 63;
+    double om2[3] = {0.0, 0.0, 0.0}, T2[3] = {0.0, 0.0, 0.0};
     // ---- phase 0: every load of the group in one round trip
     {
         // the first round's corners (issued first: the longest stream)
         {
-            const int le = wave * 4 + g;
+            const int le = wave * EPW + g;
             const int4 info = le < gne ? a.edge_info[ge0 + le] : make_int4(0, 0, 0, 0);
             if (le < gne) stage(info.z, 0, min(info.w, kGChunk));
         }
         // edge records, the group's pair lists
-        for (int t = tid; t < gne; t += 256) {
+        for (int t = tid; t < gne; t += NT) {
             sInfo[t] = a.edge_info[ge0 + t];
             sgb[t] = a.gblock[ge0 + t];
             seq[t] = a.edge_lphoto[ge0 + t];
         }
         if (tid <= np) sph0[tid] = a.photo_ptr[p0 + tid] - ge0;
-        for (int t = tid; t < nq; t += 256) spq[t] = a.gpairs[q0 + t];
-        for (int t = tid; t < nc; t += 256) scn[t] = a.gcon[c0 + t];
-        for (int t = tid; t < m; t += 256) sdg[t] = a.dg[t];
-        if (tid >= 128 && tid < 128 + C) {   // camera tables (k_linearize's wave-1 code)
-            const int c = tid - 128;
-            double om2[3], T2[3];
+        for (int t = tid; t < nq; t += NT) spq[t] = a.gpairs[q0 + t];
+        for (int t = tid; t < nc; t += NT) scn[t] = a.gcon[c0 + t];
+        for (int t = tid; t < m; t += NT) sdg[t] = a.dg[t];
+        if (tid >= CAM0 && tid < CAM0 + C) {   // camera tables: loads here, Rodrigues after the partials
+            const int c = tid - CAM0;
             if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k) { om2[k] = a.cam_rt[6 * c + k]; T2[k] = a.cam_rt[6 * c + 3 + k]; }
@@ -394,30 +399,14 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
             const int nd = a.nd;
 #pragma unroll
             for (int q = 0; q < 12; ++q) kt[6 + q] = q < nd ? (double)a.D[nd * c + q] : 0.0;
-            Rot r2;
-            rodrigues_v2m(om2, r2);
-            double J[9];
-            so3_jac(om2, r2, +1.0, J);
-            double* ct = ctab + 24 * c;
-#pragma unroll
-            for (int k = 0; k < 9; ++k) { ct[k] = r2.R[k]; ct[9 + k] = J[k]; }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) ct[18 + k] = T2[k];
-        } else if (BACK && tid == 191) {   // the double-side transform (BACK edges; DoubleSide's global block)
-            double dsr[3];
+        } else if (BACK && tid == DST) {   // the double-side transform (BACK edges; DoubleSide's global block)
             if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) { dsr[k] = a.x[k]; sds[18 + k] = a.x[3 + k]; }
+                for (int k = 0; k < 3; ++k) { om2[k] = a.x[k]; T2[k] = a.x[3 + k]; }
             } else {
 #pragma unroll
-                for (int k = 0; k < 3; ++k) { dsr[k] = a.ds_rt[k]; sds[18 + k] = a.ds_rt[3 + k]; }
+                for (int k = 0; k < 3; ++k) { om2[k] = a.ds_rt[k]; T2[k] = a.ds_rt[3 + k]; }
             }
-            Rot rd;
-            rodrigues_v2m(dsr, rd);
-            double J[9];
-            so3_jac(dsr, rd, -1.0, J);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) { sds[k] = rd.R[k]; sds[9 + k] = J[k]; }
         }
     }
     // the pending update's operands: thread (le, k) < 6 gne forms sum_i Y'_e[i][k] dg_g(e)[i]
@@ -443,7 +432,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
     __syncthreads();
     SSTAMP(stp, 1, 0);
     if (pending) {
-        for (int t = tid; t < 6 * gne; t += 256) {
+        for (int t = tid; t < 6 * gne; t += NT) {
             const int le = t / 6, k = t % 6;
             int gbl = gb0;
             double y[6];
@@ -464,6 +453,27 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
     }
     __syncthreads();
+    if (tid >= CAM0 && tid < CAM0 + C) {
+        const int c = tid - CAM0;
+        Rot r2;
+        rodrigues_v2m(om2, r2);
+        double J[9];
+        so3_jac(om2, r2, +1.0, J);
+        double* ct = ctab + 24 * c;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { ct[k] = r2.R[k]; ct[9 + k] = J[k]; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ct[18 + k] = T2[k];
+    } else if (BACK && tid == DST) {
+        Rot rd;
+        rodrigues_v2m(om2, rd);
+        double J[9];
+        so3_jac(om2, rd, -1.0, J);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { sds[k] = rd.R[k]; sds[9 + k] = J[k]; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sds[18 + k] = T2[k];
+    }
     // the photo update x = fl32(x + fl32(alpha (z' - sum_e Y'_e^T dg))) (k_prep's; src/multicalib.cpp:482-501)
     if (ptask) {
         float xn = xo;
@@ -507,7 +517,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
 
     // ---- phase A: rounds of 16 edges
     for (int rb = 0; rb < gne; rb += kGroupRound) {
-        const int es = wave * 4 + g, le = rb + es;
+        const int es = wave * EPW + g, le = rb + es;
         const bool ev = le < gne;
         const int4 info = ev ? sInfo[le] : make_int4(0, 0, 0, 0);
         const int cam = info.x;
@@ -515,10 +525,9 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         double* Gbe = sGb + 56 * es;
         if (rb > 0 && ev) stage(info.z, 0, min(info.w, kGChunk));
         if (ev) {
-            group_prologue<MODEL, BACK>(sph + 24 * seq[le], ctab + 24 * cam, sds, info.y, sub, rec + kGRec * le, P, Gbe);
+            group_prologue<MODEL, BACK, L>(sph + 24 * seq[le], ctab + 24 * cam, sds, info.y, sub, rec + kGRec * le, P, Gbe);
             const double* kt = ktab + 20 * cam;
-            P[12 + sub] = kt[sub];
-            if (sub < 2) P[28 + sub] = kt[16 + sub];
+            for (int k = sub; k < 18; k += L) P[12 + k] = kt[k];
         }
         wave_sync_lds();
         if (rb == 0) SSTAMP(stp, 3, 0);
@@ -536,7 +545,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
                 wave_sync_lds();
             }
 #pragma unroll 1
-            for (int i = sub; i < cn; i += kGroupRound) {
+            for (int i = sub; i < cn; i += L) {
                 int po = 0;
                 asm volatile("" : "+v"(po));
                 const double* Pq = P + po;
@@ -585,14 +594,14 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         if (rb == 0) SSTAMP(stp, 4, 0);
         int tq = lane;
         asm volatile("" : "+v"(tq));
-        strided_reduce_scatter<kGroupRound>(acc, tq);
-        const int gq = tq & 3, sq = tq >> 2;
-        const int base = strided_rs_base<kGroupRound>(tq);
+        strided_reduce_scatter<L>(acc, tq);
+        const int gq = tq % EPW, sq = tq / EPW;
+        const int base = strided_rs_base<L>(tq);
         wave_sync_lds();   // the corners are consumed: the chain records overwrite them
         {
             GroupChain& CW = sCH[gq];
 #pragma unroll
-            for (int q = 0; q < 32 / kGroupRound; ++q) {
+            for (int q = 0; q < 32 / L; ++q) {
                 const int idx = base + q;
                 if (idx < 21) {
                     int r, s2;
@@ -606,8 +615,8 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
         }
         wave_sync_lds();
         {
-            const int eq = rb + wave * 4 + gq;
-            group_chain(sCH[gq], sGb + 56 * (wave * 4 + gq), sq, eq < gne, rec + kGRec * (eq < gne ? eq : 0));
+            const int eq = rb + wave * EPW + gq;
+            group_chain(sCH[gq], sGb + 56 * (wave * EPW + gq), sq, eq < gne, rec + kGRec * (eq < gne ? eq : 0));
         }
         wave_sync_lds();   // this wave's chain records are consumed before the next round's corners
         if (rb == 0) SSTAMP(stp, 5, 0);
@@ -692,7 +701,7 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
     }
     __syncthreads();
     SSTAMP(stp, 8, 0);
-    for (int t = tid; t < 6 * gne; t += 256) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
+    for (int t = tid; t < 6 * gne; t += NT) {   // task (edge, row i): U row i in place of Hgp row i, Y' row i
         const int le = t / 6, i = t % 6;
         double h[6], li[36], u[6], y[6];
         double2* H2 = reinterpret_cast<double2*>(sE + ES * le + 22 + 6 * i);
@@ -727,8 +736,8 @@ __global__ __launch_bounds__(256, MCC_GROUP_OCC) void k_group(LinArgs a) {
     SSTAMP(stp, 9, 0);
     // the group's Schur pair products per camera-pair block -> its slot (k_photo's pair tasks)
     int H = 1;
-    while (H < 32 && 6 * nq * 2 * H <= 256) H *= 2;
-    for (int t = tid; t < 6 * nq * H; t += 256) {
+    while (H < 32 && 6 * nq * 2 * H <= NT) H *= 2;
+    for (int t = tid; t < 6 * nq * H; t += NT) {
         const int h = t % H, k = t / H / 6, i0 = (t / H) % 6;
         const int4 pqv = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}
         const bool diag = (pqv.z & 2) != 0;

@@ -212,13 +212,14 @@ struct ErrArgs {
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp);
 size_t mcc_solve_shmem(int m);
 hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem);
-hipError_t mcc_launch_group(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t group_shmem,
-                            hipStream_t s);
+hipError_t mcc_launch_group(const mcc::LinArgs& a, int model, bool rational, bool prism, int lanes,
+                            size_t group_shmem, hipStream_t s);
 hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
                             hipStream_t s);
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
+hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
 hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);
 hipError_t mcc_launch_peer_max(const mcc::PeerCtx& pc, mcc::State* st, double* v, hipStream_t s);

@@ -1637,7 +1637,7 @@ __device__ __forceinline__ double dpp_f64u(double v) {   // no 'old' operand to 
 }
 template <int L>
 __device__ __forceinline__ void strided_reduce_scatter(double* v, int lane) {
-    static_assert(L == 16 || L == 8, "lanes per edge");
+    static_assert(L == 32 || L == 16 || L == 8, "lanes per edge");
 #pragma unroll
     for (int j = 0; j < 16; ++j) { double p = v[j], q = v[j + 16]; pl32_swap(p, q); v[j] = p + q; }   // lane ^ 32
 #pragma unroll
@@ -1650,7 +1650,7 @@ __device__ __forceinline__ void strided_reduce_scatter(double* v, int lane) {
             v[j] = keep + dpp_f64u<kDppRor8>(send);
         }
     }
-    if (L == 16) {   // lane ^ 4: i - 4 for the upper, i + 4 = i - 12 for the lower
+    if (L >= 16) {   // lane ^ 4: i - 4 for the upper, i + 4 = i - 12 for the lower
         const bool hi = (lane & 4) != 0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1659,10 +1659,16 @@ __device__ __forceinline__ void strided_reduce_scatter(double* v, int lane) {
             v[j] = keep + (hi ? p4 : p12);
         }
     }
+    if (L == 32) {   // lane ^ 2: a quad permutation
+        const bool hi = (lane & 2) != 0;
+        const double send = hi ? v[0] : v[1], keep = hi ? v[1] : v[0];
+        v[0] = keep + dpp_f64u<kDppXor2>(send);
+    }
 }
 template <int L>
 __device__ __forceinline__ int strided_rs_base(int lane) {
-    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + (L == 16 ? 2 * ((lane >> 2) & 1) : 0);
+    return 16 * ((lane >> 5) & 1) + 8 * ((lane >> 4) & 1) + 4 * ((lane >> 3) & 1) + (L >= 16 ? 2 * ((lane >> 2) & 1) : 0) +
+           (L == 32 ? ((lane >> 1) & 1) : 0);
 }
 // packed upper index t < 21 -> (r, s), r <= s, without a loop: r from a 3-bit-per-entry table
 __device__ __forceinline__ void tri6(int t, int& r, int& s) {
@@ -2346,17 +2352,36 @@ __device__ __forceinline__ double gjb_bcast16(double v) {
 // every lane by DPP row_newbcast:K inside each 16-lane row (the lanes of one column group), A[i][K]
 // of each row by one bpermute; then A[i][j] -= f A[K][j] with f = A[i][K] ip, the pivot row is
 // scaled by ip, and column K becomes -f (ip on the diagonal).
+// Row group GK (16 lanes) of x copied to every row group: lane (i, g) gets x(i, GK).  Two VALU
+// swaps (v_permlane16_swap: odd rows <-> even rows, v_permlane32_swap: halves), no LDS path.
+template <int GK>
+__device__ __forceinline__ double bcast_group(double x) {
+    double a = x, b = x;
+    pl16_swap(a, b);                      // a(i, g) = x(i, g & ~1), b(i, g) = x(i, g | 1)
+    double c = (GK & 1) ? b : a;          // c(i, g) = x(i, (g & 2) | (GK & 1))
+    double d = c, e = c;
+    pl32_swap(d, e);                      // d(i, g) = c(i, g & 1), e(i, g) = c(i, 2 | (g & 1))
+    return (GK & 2) ? e : d;
+}
+#ifndef MCC_GJB_SWAP
+#define MCC_GJB_SWAP 1   // 0: the pivot column by ds_bpermute and the pivot by v_readlane (A/B)
+#endif
 template <int K>
 struct GjbStep {
     __device__ __forceinline__ static void run(double (&v)[4], int lane, bool& ok) {
         constexpr int gk = K >> 2, ck = K & 3;
+        const int i = lane & 15, g = lane >> 4;
+#if MCC_GJB_SWAP
+        const double rik = bcast_group<gk>(v[ck]);     // row i's column-K entry
+        const double piv = gjb_bcast16<K>(rik);          // row K's: the pivot
+#else
         const double piv = readlane_f64(v[ck], K + 16 * gk);
+        const double rik = __shfl(v[ck], i + 16 * gk);   // row i's column-K entry
+#endif
         ok &= piv > 0.0;
         const double pv = piv > 0.0 ? piv : 1.0;
         double ip = __builtin_amdgcn_rcp(pv);
         ip = fma(ip, fma(-pv, ip, 1.0), ip);
-        const int i = lane & 15, g = lane >> 4;
-        const double rik = __shfl(v[ck], i + 16 * gk);   // row i's column-K entry
         const bool prow = i == K;
         // other rows: v - f pr with f = A[i][K] ip; the pivot row (pr = its own v): fma(ip, v, 0), an
         // exactly rounded v ip (1 - ip and a difference would cancel when ip is tiny)
@@ -2390,13 +2415,11 @@ __device__ __forceinline__ bool gjb_inverse16(const double* Pk, int ld, double* 
     for (int c = 0; c < 4; ++c) v[c] = Pk[i * ld + 4 * g + c];
     return gjb_inverse16_regs(v, PV, lane);
 }
-#ifdef MCC_GJB_STAMPS
-__device__ long long g_gjb_stamps[64];
-#define GJB_STAMP(k) do { if (threadIdx.x == 0) g_gjb_stamps[k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define GJB_STAMP(k) do { } while (0)
-#endif
-__device__ __forceinline__ void gj_blocked(const double* packed, double* x, double* A, double* PV, int m, int* err) {
+// gst (mcc_debug_solve only; null in the step kernels): s_memtime of thread 0 at the phase
+// boundaries, slot 0 after the loads, 1 + 3 kb .. 3 + 3 kb per pivot block step
+#define GJB_STAMP(k) do { if (gst && threadIdx.x == 0) gst[k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
+__device__ __forceinline__ void gj_blocked(const double* packed, double* x, double* A, double* PV, int m, int* err,
+                                           long long* gst) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int nb = (m + 15) / 16, M = 16 * nb, ld = M + 1, ntri = m * (m + 1) / 2;
     // rhs, padding and the packed triangle: every global load is issued before the first LDS store
@@ -2568,7 +2591,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     SSTAMP(a.stamps, 4, 0);
     if (LARGE) {   // S is the packed system itself (global); r (LDS) is followed by the block work area
         const int M = 16 * ((m + 15) / 16);
-        gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error);
+        gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error, nullptr);
     }
     SSTAMP(a.stamps, 5, 0);
     if (tid < 64) {
@@ -2770,6 +2793,19 @@ __global__ __launch_bounds__(1024) void k_solve(SolveArgs a) {
     for (int t = tid; t < m; t += blockDim.x) r[t] = a.packed[ntri + t];
     __syncthreads();
     solve_global<false>(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+}
+
+// ---------------------------------------------------------------- mcc_debug_solve
+// The m > 30 dense solve alone (k_solve's elimination on a packed SPD system [S upper | r]):
+// x = S^-1 r, the error bits, and per-phase stamps.  Test and measurement only.
+__global__ __launch_bounds__(1024) void k_debug_solve(const double* packed, double* xout, int m, int* err,
+                                                       long long* gst) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int M = 16 * ((m + 15) / 16);
+    gj_blocked(packed, sm, sm + M, sm + M + M * (M + 1), m, err, gst);
+    __syncthreads();
+    GJB_STAMP(63);
+    for (int t = threadIdx.x; t < m; t += blockDim.x) xout[t] = sm[t];
 }
 
 // ---------------------------------------------------------------- peer transport: handshake, max
@@ -3061,43 +3097,56 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-template <int MODEL, bool RATIONAL, bool PRISM, bool BACK>
+template <int MODEL, bool RATIONAL, bool PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
-    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK>), dim3(a.n_pgroups), dim3(256), shmem, s, a);
+    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), dim3(a.n_pgroups), dim3(kGroupRound * L), shmem, s, a);
     return hipGetLastError();
 }
-hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, bool prism, size_t shmem, hipStream_t s) {
-    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
-    if (model == MCC_MODEL_OMNI) return launch_group_t<MCC_MODEL_OMNI, false, false, false>(a, shmem, s);
+template <int L>
+static hipError_t launch_group_l(const LinArgs& a, int model, bool rational, bool prism, size_t shmem, hipStream_t s) {
+    if (model == MCC_MODEL_OMNI) return launch_group_t<MCC_MODEL_OMNI, false, false, false, L>(a, shmem, s);
     if (model == MCC_MODEL_DOUBLESIDE) {
-        if (rational && prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, true, true>(a, shmem, s);
-        if (rational) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, false, true>(a, shmem, s);
-        if (prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, false, true, true>(a, shmem, s);
-        return launch_group_t<MCC_MODEL_DOUBLESIDE, false, false, true>(a, shmem, s);
+        if (rational && prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, true, true, L>(a, shmem, s);
+        if (rational) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, false, true, L>(a, shmem, s);
+        if (prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, false, true, true, L>(a, shmem, s);
+        return launch_group_t<MCC_MODEL_DOUBLESIDE, false, false, true, L>(a, shmem, s);
     }
     if (a.has_back) {
-        if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, true>(a, shmem, s);
-        if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, true>(a, shmem, s);
-        if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, true>(a, shmem, s);
-        return launch_group_t<MCC_MODEL_PINHOLE, false, false, true>(a, shmem, s);
+        if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, true, L>(a, shmem, s);
+        if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, true, L>(a, shmem, s);
+        if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, true, L>(a, shmem, s);
+        return launch_group_t<MCC_MODEL_PINHOLE, false, false, true, L>(a, shmem, s);
     }
-    if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, false>(a, shmem, s);
-    if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, false>(a, shmem, s);
-    if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, false>(a, shmem, s);
-    return launch_group_t<MCC_MODEL_PINHOLE, false, false, false>(a, shmem, s);
+    if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, false, L>(a, shmem, s);
+    if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, false, L>(a, shmem, s);
+    if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, false, L>(a, shmem, s);
+    return launch_group_t<MCC_MODEL_PINHOLE, false, false, false, L>(a, shmem, s);
+}
+hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, bool prism, int lanes, size_t shmem,
+                            hipStream_t s) {
+    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
+    return lanes == 32 ? launch_group_l<32>(a, model, rational, prism, shmem, s)
+                       : launch_group_l<16>(a, model, rational, prism, shmem, s);
+}
+template <int L>
+static hipError_t set_group_attrs(size_t group_shmem) {
+    hipError_t err = hipSuccess;
+#define SETG(M, R, P, B) hipFuncSetAttribute((const void*)&k_group<M, R, P, B, L>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_shmem)
+    for (hipError_t e : {SETG(1, false, false, false), SETG(2, true, true, true), SETG(2, true, false, true),
+                         SETG(2, false, true, true), SETG(2, false, false, true), SETG(0, true, true, true),
+                         SETG(0, true, false, true), SETG(0, false, true, true), SETG(0, false, false, true),
+                         SETG(0, true, true, false), SETG(0, true, false, false), SETG(0, false, true, false),
+                         SETG(0, false, false, false)})
+        if (e != hipSuccess) err = e;
+#undef SETG
+    return err;
 }
 
 hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem) {
     hipError_t err = hipSuccess;
     if (group_shmem > 64 * 1024) {
-#define SETG(M, R, P, B) hipFuncSetAttribute((const void*)&k_group<M, R, P, B>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_shmem)
-        for (hipError_t e : {SETG(1, false, false, false), SETG(2, true, true, true), SETG(2, true, false, true),
-                             SETG(2, false, true, true), SETG(2, false, false, true), SETG(0, true, true, true),
-                             SETG(0, true, false, true), SETG(0, false, true, true), SETG(0, false, false, true),
-                             SETG(0, true, true, false), SETG(0, true, false, false), SETG(0, false, true, false),
-                             SETG(0, false, false, false)})
+        for (hipError_t e : {set_group_attrs<16>(group_shmem), set_group_attrs<32>(group_shmem)})
             if (e != hipSuccess) err = e;
-#undef SETG
     }
     const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, max_cpp);
     if (shmem > 64 * 1024) {
@@ -3133,6 +3182,13 @@ hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
     // m > 30: 8 waves, so the block eliminations of a pivot step (up to (nb - 1)^2 16 x 16 MFMA
     // products) are not what waits on the next pivot inverse
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(a.ctx.m > 30 ? kSolveThreads : 256), mcc_solve_shmem(a.ctx.m), s, a);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s) {
+    const size_t shm = mcc_solve_shmem(m);
+    hipError_t e = hipFuncSetAttribute((const void*)&k_debug_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_debug_solve, dim3(1), dim3(kSolveThreads), shm, s, packed, x, m, err, stamps);
     return hipGetLastError();
 }
 hipError_t mcc_launch_peer_handshake(const PeerCtx& pc, State* st, double* out, hipStream_t s) {

@@ -72,6 +72,11 @@ for _n in SPLIT:
 for _n in ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd12_prism"]:
     CASES[_n + "_split3"] = CASES[_n]
 CASES["config3_small_split3"] = CASES["config3_small"]
+# k_group at both lane widths: "_g16" its 256-thread form (16 lanes per edge), "_g32" the default
+# 512-thread form forced where the rig's groups outnumber the CUs (MCC_GROUP=1)
+for _n in ["config4_small", "pinhole_back", "omni_skew"]:
+    CASES[_n + "_g16"] = CASES[_n]
+CASES["config3_small_g32"] = CASES["config3_small"]
 
 
 def make_adjuster(name, p):
@@ -80,6 +85,10 @@ def make_adjuster(name, p):
         env = {"MCC_FUSED": "0"}
     elif name.endswith("_split3"):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "0"}
+    elif name.endswith("_g16"):
+        env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "16"}
+    elif name.endswith("_g32"):
+        env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "32"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -96,6 +105,15 @@ def make_adjuster(name, p):
 def case(request):
     p = CASES[request.param]()
     return request.param, p, O.Oracle(p), make_adjuster(request.param, p)
+
+
+def test_forced_step_kernels(case):
+    """The A/B suffixes reach the linearisation kernels they name (mcc_problem_path)."""
+    name, p, o, g = case
+    want = {"_split3": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group"}
+    for suf, k in want.items():
+        if name.endswith(suf):
+            assert g.step_kernels() == k, name
 
 
 def test_residuals_bitwise(case):
