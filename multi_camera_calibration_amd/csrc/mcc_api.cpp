@@ -166,6 +166,13 @@ struct mcc_problem {
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
     DevBuf<int> pgrp_ptr, pgrp_edge, gpair_ptr, gcon_ptr;
+    DevBuf<int> prep_ptr, prep_edge;   // k_prep4's groups (three-kernel split step)
+    // MCC_POISON_HANDOFF=1 (test): every buffer handed between workgroups inside one launch or
+    // between the step's kernels is filled with NaN (all-ones bytes) before each step, so that a
+    // read of a word its producer has not yet stored this step shows up in the result
+    bool poison = false;
+    int poison_level = 0;
+    int n_prep = 0, prep_lanes = 1;   // MCC_PREP_LANES=4: k_prep4 (measured slower at configs 3 and 5)
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
@@ -237,6 +244,15 @@ mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
 int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     using namespace mcc;
     const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
+    if (p->poison) {
+        for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed})
+            if (b->p && b->n) HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
+        for (auto* b : {&p->erec, &p->echain, &p->eh})
+            if (b->p && b->n) HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
+        // 2: the negative control -- dg carries the previous solve into this step's photo update,
+        // so poisoning it must reach the parameters (the test checks that it does)
+        if (p->poison_level > 1 && p->dg.p) HIPCHK(hipMemsetAsync(p->dg.p, 0xFF, sizeof(double) * p->dg.n, p->stream));
+    }
     if (tim) HIPCHK(hipEventRecord(p->ev_step[p->ev_used], p->stream));
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used], p->stream));
     LinArgs la{};
@@ -255,6 +271,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.Y = p->Y.p; la.zp = p->zp.p;
     la.pgrp_ptr = p->pgrp_ptr.p; la.pgrp_edge = p->pgrp_edge.p; la.edge_lphoto = p->edge_lphoto.p; la.gpair_ptr = p->gpair_ptr.p; la.gpairs = p->gpairs.p;
     la.gcon_ptr = p->gcon_ptr.p; la.gcon = p->gcon.p; la.pairprod = p->pairprod.p;
+    la.prep_ptr = p->prep_ptr.p; la.prep_edge = p->prep_edge.p; la.n_prep = p->n_prep; la.prep_lanes = p->prep_lanes;
     la.n_pgroups = p->n_pgroups; la.max_gpairs = p->max_gpairs; la.max_gcon = p->max_gcon; la.max_gedges = p->max_gedges;
     la.gp_tot = p->gp_tot.p;
     la.resid = resid_dev;
@@ -594,6 +611,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
     if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);
     if (const char* f = std::getenv("MCC_GROUP_LANES")) p->group_lanes = std::atoi(f) == 16 ? 16 : 32;
+    if (const char* f = std::getenv("MCC_POISON_HANDOFF")) {
+        p->poison_level = std::atoi(f);
+        p->poison = p->poison_level != 0;
+    }
     const int NG = (int)pgrp_ptr.size() - 1;
     std::vector<int4> gpairs;                           // {first contribution, count, diagonal << 1, slot}
     std::vector<unsigned> gcon;
@@ -747,6 +768,26 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
                 for (int e = photo_ptr[v]; e < photo_ptr[v + 1]; ++e) lph[e] = (unsigned char)(v - pgrp_ptr[g]);
         HIPC(p->edge_lphoto.upload(lph.data(), lph.size()));
     }
+    if (!p->fused && !p->use_group) {
+        // k_prep4's groups: consecutive photos, <= kPrepPhotos of them and kPrepEdges edges (or one photo)
+        if (const char* f = std::getenv("MCC_PREP_LANES")) p->prep_lanes = std::atoi(f) == 4 ? 4 : 1;
+        std::vector<int> pp(1, 0);
+        for (int v = 0; v < V;) {
+            int w = v, edges = 0;
+            while (w < V && w - v < mcc::kPrepPhotos &&
+                   (w == v || edges + (photo_ptr[w + 1] - photo_ptr[w]) <= mcc::kPrepEdges)) {
+                edges += photo_ptr[w + 1] - photo_ptr[w];
+                ++w;
+            }
+            pp.push_back(w);
+            v = w;
+        }
+        std::vector<int> pe(pp.size());
+        for (size_t g = 0; g < pp.size(); ++g) pe[g] = photo_ptr[pp[g]];
+        p->n_prep = (int)pp.size() - 1;
+        HIPC(p->prep_ptr.upload(pp.data(), pp.size()));
+        HIPC(p->prep_edge.upload(pe.data(), pe.size()));
+    }
     HIPC(p->gpair_ptr.upload(gpair_ptr.data(), gpair_ptr.size()));
     HIPC(p->gpairs.upload(gpairs.data(), gpairs.size()));
     HIPC(p->gcon_ptr.upload(gcon_ptr.data(), gcon_ptr.size()));
@@ -829,6 +870,7 @@ void mcc_destroy(mcc_problem* p) {
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->gpairs.release();
+    p->prep_ptr.release(); p->prep_edge.release();
     p->pgrp_ptr.release(); p->pgrp_edge.release(); p->edge_lphoto.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);

@@ -28,7 +28,7 @@
 // src/mymulticalib.cpp:546-553; the chain maps), with lanes owning the entries of each 3x3
 // product.  S: 84 doubles of scratch.  Outputs: P[0..11] = R, T of the float32 pose; Gb = the
 // chain maps' nonzero blocks [Gp11, Gp21, Gp22 | pad | Gg11, Gg21, Gg22 | pad].
-template <int MODEL, bool BACK, int L>
+template <int MODEL, bool BACK, int L, int GW = 28>
 __device__ __forceinline__ void group_prologue(const double* ph, const double* ct, const double* sds, int side,
                                                int sub, double* S, double* P, double* Gb) {
     const double* R1 = ph;
@@ -40,14 +40,16 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
     double* X = S;        // R3 [0..8], T3 [9..11], q [12..14]
     double* W = S + 15;   // A1 [0..8], A2 [9..17], B2 [18..26]
     // ---- compose_motion(photo, camera): R3 = R2 R1, q = R2 T1, T3 = q + T2 (OpenCV order)
-    if (sub < 9) {
-        const int i = sub / 3, j = sub % 3;
-        X[sub] = dot3_nc(R2[i * 3], R1[j], R2[i * 3 + 1], R1[3 + j], R2[i * 3 + 2], R1[6 + j]);
-    } else if (sub < 12) {
-        const int i = sub - 9;
-        const double q = dot3_nc(R2[i * 3], T1[0], R2[i * 3 + 1], T1[1], R2[i * 3 + 2], T1[2]);
-        X[12 + i] = q;
-        X[9 + i] = add_nc(q, T2[i]);
+    for (int e = sub; e < 12; e += L) {
+        if (e < 9) {
+            const int i = e / 3, j = e % 3;
+            X[e] = dot3_nc(R2[i * 3], R1[j], R2[i * 3 + 1], R1[3 + j], R2[i * 3 + 2], R1[6 + j]);
+        } else {
+            const int i = e - 9;
+            const double q = dot3_nc(R2[i * 3], T1[0], R2[i * 3 + 1], T1[1], R2[i * 3 + 2], T1[2]);
+            X[12 + i] = q;
+            X[9 + i] = add_nc(q, T2[i]);
+        }
     }
     wave_sync_lds();
     double om[3], th, sn, cs;
@@ -103,7 +105,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
             } else {
                 v = w == 0 ? R2[ee] : (i == j ? 1.0 : 0.0);
             }
-            Gb[28 * w + 9 * blk + ee] = v;
+            Gb[GW * w + 9 * blk + ee] = v;
         }
         return;
     }
@@ -115,14 +117,16 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
     const double* Rds = sds;
     const double* Jrds = sds + 9;
     const double* dst = sds + 18;
-    if (sub < 9) {
-        const int i = sub / 3, j = sub % 3;
-        Xb[sub] = dot3_nc(X[i * 3], Rds[j], X[i * 3 + 1], Rds[3 + j], X[i * 3 + 2], Rds[6 + j]);
-    } else if (sub < 12) {
-        const int i = sub - 9;
-        const double q = dot3_nc(X[i * 3], dst[0], X[i * 3 + 1], dst[1], X[i * 3 + 2], dst[2]);
-        Xb[12 + i] = q;
-        Xb[9 + i] = add_nc(q, X[9 + i]);
+    for (int e = sub; e < 12; e += L) {
+        if (e < 9) {
+            const int i = e / 3, j = e % 3;
+            Xb[e] = dot3_nc(X[i * 3], Rds[j], X[i * 3 + 1], Rds[3 + j], X[i * 3 + 2], Rds[6 + j]);
+        } else {
+            const int i = e - 9;
+            const double q = dot3_nc(X[i * 3], dst[0], X[i * 3 + 1], dst[1], X[i * 3 + 2], dst[2]);
+            Xb[12 + i] = q;
+            Xb[9 + i] = add_nc(q, X[9 + i]);
+        }
     }
     wave_sync_lds();
     double omb[3], thb, snb, csb;
@@ -187,7 +191,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         } else {
             v = w == 0 ? R2[ee] : (ds ? X[ee] : (i == j ? 1.0 : 0.0));
         }
-        Gb[28 * w + 9 * blk + ee] = v;
+        Gb[GW * w + 9 * blk + ee] = v;
     }
 }
 
@@ -800,4 +804,172 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     __syncthreads();
     SSTAMP(stp, 10, 0);
 #endif
+}
+
+// ---------------------------------------------------------------- k_prep4
+// The three-kernel split step's first kernel (k_prep -> k_edge -> k_photo) with the edge prologue
+// spread over 4 lanes: one wave per group of consecutive photos (at most kPrepPhotos photos and
+// kPrepEdges edges, or one photo with more, in rounds of 16 edges), doing
+//   - every load in one round trip after the group's ranges (k_group's phase 0: dg, the cameras,
+//     the photos' x and z', the edge records, the first Y' column of each (edge, k) task);
+//   - the pending photo update x = fl32(x + fl32(alpha (z' - sum_e Y'_e^T dg))) in edge order
+//     (k_prep's; src/multicalib.cpp:482-501) and the stop test's norm partials;
+//   - one Rodrigues pass over the photos, the cameras and the double-side transform (lanes
+//     running the same code on different poses);
+//   - group_prologue by 4 lanes per edge (lanes own entries of the 3 x 3 products; the scalar
+//     chain -- m2v, the float32 pose's Rodrigues, the Jacobian coefficients -- per lane), writing
+//     erec (R, T) and echain (the chain maps' nonzero blocks) for k_edge.
+// One lane per edge (k_prep, prep_lanes = 1) leaves the matrix work of an edge on one lane; four
+// lanes cut each wave's instruction stream and write each record 4 doubles per edge at a time.
+#ifndef MCC_PREP4_WAVES
+#define MCC_PREP4_WAVES 2
+#endif
+template <int MODEL, bool BACK>
+__global__ __launch_bounds__(64, MCC_PREP4_WAVES) void k_prep4(LinArgs a) {
+    const State* st = a.state;
+    const int tid = threadIdx.x, grp = blockIdx.x;
+    const int done = st->done, pending = st->pending;
+    const double alpha_prev = st->alpha;   // step factor of the pending update
+    const int p0 = a.prep_ptr[grp], np = a.prep_ptr[grp + 1] - p0;
+    const int ge0 = a.prep_edge[grp], gne = a.prep_edge[grp + 1] - ge0;
+    if (done) return;
+    long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)grp + 8 : nullptr;   // MCC_DIAG: slots 8..11
+    SSTAMP(stp, 0, 0);
+    const int C = a.n_cams, m = a.global_dim;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const PrepLayout PL = prep_layout(C, BACK);
+    double* tab = smem + PL.tab;     // photos [0, kPrepPhotos), cameras, the double-side transform
+    double* S = smem + PL.S;
+    double* spart = S;               // the update's partial sums (consumed before the prologues)
+    double* sdg = smem + PL.sdg;
+    double* sxn = smem + PL.sxn;
+    double* scam = smem + PL.scam;   // camera (rvec, tvec) [6C], the double-side transform [6]
+    int* ib = reinterpret_cast<int*>(smem + PL.ndoubles);
+    int4* sInfo = reinterpret_cast<int4*>(ib + PL.iInfo);
+    int* sgb = ib + PL.iGb;
+    int* sph0 = ib + PL.iPh;
+    constexpr int SW = BACK ? 84 : 42;
+    // ---- phase 0: one round trip
+    for (int t = tid; t < m; t += 64) sdg[t] = a.dg[t];
+    for (int t = tid; t < 6 * C; t += 64) {
+        const int c = t / 6, k = t % 6;
+        scam[t] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.cam_rt[t]
+                                                : (c == 0 ? 0.0 : (double)a.x[6 * (c - 1) + k]);   // src/mymulticalib.cpp:721-725
+    }
+    if (BACK && tid < 6) scam[6 * C + tid] = MODEL == MCC_MODEL_DOUBLESIDE ? (double)a.x[tid] : a.ds_rt[tid];
+    if (tid <= np) sph0[tid] = a.photo_ptr[p0 + tid] - ge0;
+    for (int t = tid; t < gne; t += 64) {
+        sInfo[t] = a.edge_info[ge0 + t];
+        sgb[t] = a.gblock[ge0 + t];
+    }
+    const int pq = tid / 6, pk = tid % 6;
+    const bool ptask = pq < np;
+    float xo = 0.f;
+    double zk = 0.0;
+    if (ptask) {
+        xo = a.x[m + 6 * (size_t)(p0 + pq) + pk];
+        if (pending) zk = a.zp[6 * (size_t)(p0 + pq) + pk];
+    }
+    double y0[6];
+    int gb0 = -1;
+    if (pending && tid < 6 * gne) {
+        const int le = tid / 6, k = tid % 6;
+        gb0 = a.gblock[ge0 + le];
+        const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) y0[i] = Ye[6 * i + k];
+    }
+    wave_sync_lds();
+    // ---- the pending update: (edge, k) partials, then photo q's component k in edge order
+    if (pending) {
+        for (int t = tid; t < 6 * gne; t += 64) {
+            const int le = t / 6, k = t % 6;
+            int gbl = gb0;
+            double y[6];
+            if (t == tid) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y[i] = y0[i];
+            } else {
+                gbl = sgb[le];
+                const double* Ye = a.Y + 36 * (size_t)(ge0 + le);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) y[i] = Ye[6 * i + k];
+            }
+            const double* d = sdg + 6 * (gbl < 0 ? 0 : gbl);
+            double sk = 0.0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) sk += y[i] * d[i];
+            spart[6 * le + k] = gbl < 0 ? 0.0 : sk;
+        }
+    }
+    wave_sync_lds();
+    if (ptask) {
+        float xn = xo;
+        double Gk = 0.0;
+        if (pending) {
+            double t = zk;
+            for (int le = sph0[pq]; le < sph0[pq + 1]; ++le) t -= spart[6 * le + pk];
+            const float G = (float)(alpha_prev * t);   // G = alpha*delta -> CV_32F (:491-496)
+            xn = xo + G;                                // x = x + G (:501)
+            a.x[m + 6 * (size_t)(p0 + pq) + pk] = xn;
+            Gk = (double)G;
+        }
+        sxn[16 * pq + pk] = (double)xn;
+        sxn[16 * pq + 8 + pk] = Gk;
+    }
+    wave_sync_lds();
+    SSTAMP(stp, 1, 0);
+    if (pending && ptask && pk == 0) {   // ||G||^2, ||x||^2 partials of the applied update (stop test)
+        const double* xs = sxn + 16 * pq;
+        double g2 = 0.0, x2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            g2 += xs[8 + q] * xs[8 + q];
+            x2 += xs[q] * xs[q];
+        }
+        a.photo_norm[2 * (size_t)(p0 + pq)] = g2;
+        a.photo_norm[2 * (size_t)(p0 + pq) + 1] = x2;
+    }
+    // ---- one Rodrigues pass: photos (Jr), cameras (Jl), the double-side transform (Jr)
+    for (int t = tid; t < np + C + (BACK ? 1 : 0); t += 64) {
+        const double* src;
+        double* out;
+        double sgn;
+        if (t < np) {
+            src = sxn + 16 * t; out = tab + 24 * t; sgn = -1.0;
+        } else if (t < np + C) {
+            src = scam + 6 * (t - np); out = tab + 24 * (kPrepPhotos + t - np); sgn = 1.0;
+        } else {
+            src = scam + 6 * C; out = tab + 24 * (kPrepPhotos + C); sgn = -1.0;
+        }
+        const double om[3] = {src[0], src[1], src[2]};
+        Rot r;
+        rodrigues_v2m(om, r);
+        double J[9];
+        so3_jac(om, r, sgn, J);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { out[k] = r.R[k]; out[9 + k] = J[k]; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) out[18 + k] = src[3 + k];
+    }
+    wave_sync_lds();
+    SSTAMP(stp, 2, 0);
+    // ---- the edge prologues: rounds of 16 edges, 4 lanes each -> erec, echain
+    const int es = tid >> 2, sub = tid & 3;
+    for (int rb = 0; rb < gne; rb += kPrepEdges) {
+        const int le = rb + es;
+        if (le < gne) {
+            const int4 info = sInfo[le];
+            int q = 0;
+            while (q + 1 < np && sph0[q + 1] <= le) ++q;
+            const size_t e = (size_t)ge0 + le;
+            group_prologue<MODEL, BACK, 4, 27>(tab + 24 * q, tab + 24 * (kPrepPhotos + info.x), tab + 24 * (kPrepPhotos + C),
+                                               info.y, sub, S + SW * es, a.erec + 12 * e, a.echain + 54 * e);
+        }
+        wave_sync_lds();   // this round's scratch is consumed before the next round's
+    }
+#ifdef MCC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SSTAMP(stp, 3, 0);
 }

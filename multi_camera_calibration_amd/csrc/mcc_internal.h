@@ -101,6 +101,10 @@ struct LinArgs {
     double* erec;            // [12E] R (9), T (3) of the float32 composed pose (k_prep -> k_edge)
     double* echain;          // [54E] chain-map blocks Gp11, Gp21, Gp22, Gg11, Gg21, Gg22 (k_prep -> k_edge)
     double* eh;              // [90E] Hpp upper (21), Hgg upper (21), Hgp (36), gp (6), gg (6) (k_edge -> k_photo)
+    // k_prep4: groups of consecutive photos (<= kPrepPhotos photos and kPrepEdges edges, or one photo)
+    const int* prep_ptr;     // [n_prep + 1] first photo of each group
+    const int* prep_edge;    // [n_prep + 1] first edge of each group
+    int n_prep, prep_lanes;  // prep_lanes: 4 (k_prep4) or 1 (k_prep, one lane per edge)
 };
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
@@ -156,6 +160,37 @@ __host__ __device__ inline GroupLayout group_layout(int gne, int C, int nq, int 
 }
 __host__ __device__ inline size_t group_lds_bytes(int gne, int C, int nq, int nc) {
     const GroupLayout L = group_layout(gne, C, nq, nc);
+    return (size_t)L.ndoubles * 8 + (size_t)L.nints * 4;
+}
+
+// k_prep4 (mcc_group.hpp): one wave per group of consecutive photos, 4 lanes per edge prologue
+constexpr int kPrepEdges = 16;            // edges per round (64 lanes / 4); the groups' edge cap
+constexpr int kPrepPhotos = kPhotoGroup;  // photos per group, at most
+struct PrepLayout {
+    int tab, S, sdg, sxn, scam, ndoubles;   // doubles
+    int iInfo, iGb, iPh, nints;             // ints after the doubles
+};
+// tab: Rodrigues tables (R 9, J 9, T 3, pad) of the photos [kPrepPhotos], cameras [C] and the
+// double-side transform; S: per edge slot the prologue's scratch (84 doubles with back-side
+// edges, else 42), aliased by the photo update's partial sums (<= 64 edges x 6)
+__host__ __device__ inline PrepLayout prep_layout(int C, bool back) {
+    PrepLayout L;
+    int o = 0;
+    L.tab = o; o += 24 * (kPrepPhotos + C + 1);
+    L.S = o; o += kPrepEdges * (back ? 84 : 42);
+    L.sdg = o; o += 128;
+    L.sxn = o; o += 16 * kPrepPhotos;
+    L.scam = o; o += 6 * C + 6;
+    L.ndoubles = (o + 1) & ~1;
+    int n = 0;
+    L.iInfo = n; n += 4 * 64;
+    L.iGb = n; n += 64;
+    L.iPh = n; n += kPrepPhotos + 1;
+    L.nints = n;
+    return L;
+}
+__host__ __device__ inline size_t prep_lds_bytes(int C, bool back) {
+    const PrepLayout L = prep_layout(C, back);
     return (size_t)L.ndoubles * 8 + (size_t)L.nints * 4;
 }
 

@@ -3054,17 +3054,25 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, bool pri
                             hipStream_t s) {
     if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
     const dim3 gp((a.n_photos + 64 / kPrepGroup - 1) / (64 / kPrepGroup));
+    const bool p4 = a.prep_lanes == 4;
+    const bool back = model == MCC_MODEL_DOUBLESIDE || (model == MCC_MODEL_PINHOLE && a.has_back);
+    const size_t p4shm = prep_lds_bytes(a.n_cams, back);
+    const dim3 g4(a.n_prep);
     if (model == MCC_MODEL_OMNI) {
-        hipLaunchKernelGGL((k_prep<MCC_MODEL_OMNI, false>), gp, dim3(64), 0, s, a);
+        if (p4) hipLaunchKernelGGL((k_prep4<MCC_MODEL_OMNI, false>), g4, dim3(64), p4shm, s, a);
+        else hipLaunchKernelGGL((k_prep<MCC_MODEL_OMNI, false>), gp, dim3(64), 0, s, a);
         launch_edge<MCC_MODEL_OMNI, false, false>(a, s);
     } else if (model == MCC_MODEL_DOUBLESIDE) {
-        hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE, true>), gp, dim3(64), 0, s, a);
+        if (p4) hipLaunchKernelGGL((k_prep4<MCC_MODEL_DOUBLESIDE, true>), g4, dim3(64), p4shm, s, a);
+        else hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE, true>), gp, dim3(64), 0, s, a);
         if (rational && prism) launch_edge<MCC_MODEL_DOUBLESIDE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_DOUBLESIDE, true, false>(a, s);
         else if (prism) launch_edge<MCC_MODEL_DOUBLESIDE, false, true>(a, s);
         else launch_edge<MCC_MODEL_DOUBLESIDE, false, false>(a, s);
     } else {
-        if (a.has_back) hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, true>), gp, dim3(64), 0, s, a);
+        if (p4 && a.has_back) hipLaunchKernelGGL((k_prep4<MCC_MODEL_PINHOLE, true>), g4, dim3(64), p4shm, s, a);
+        else if (p4) hipLaunchKernelGGL((k_prep4<MCC_MODEL_PINHOLE, false>), g4, dim3(64), p4shm, s, a);
+        else if (a.has_back) hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, true>), gp, dim3(64), 0, s, a);
         else hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, false>), gp, dim3(64), 0, s, a);
         if (rational && prism) launch_edge<MCC_MODEL_PINHOLE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_PINHOLE, true, false>(a, s);

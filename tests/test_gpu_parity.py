@@ -77,6 +77,9 @@ CASES["config3_small_split3"] = CASES["config3_small"]
 for _n in ["config4_small", "pinhole_back", "omni_skew"]:
     CASES[_n + "_g16"] = CASES[_n]
 CASES["config3_small_g32"] = CASES["config3_small"]
+# the three-kernel step's k_prep4 (4 lanes per edge prologue, MCC_PREP_LANES=4; default k_prep, one lane)
+for _n in ["config3_small", "pinhole_back", "config5_small"]:
+    CASES[_n + "_prep4"] = CASES[_n]
 
 
 def make_adjuster(name, p):
@@ -85,6 +88,8 @@ def make_adjuster(name, p):
         env = {"MCC_FUSED": "0"}
     elif name.endswith("_split3"):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "0"}
+    elif name.endswith("_prep4"):
+        env = {"MCC_FUSED": "0", "MCC_GROUP": "0", "MCC_PREP_LANES": "4"}
     elif name.endswith("_g16"):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "16"}
     elif name.endswith("_g32"):
@@ -110,7 +115,7 @@ def case(request):
 def test_forced_step_kernels(case):
     """The A/B suffixes reach the linearisation kernels they name (mcc_problem_path)."""
     name, p, o, g = case
-    want = {"_split3": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group"}
+    want = {"_split3": "k_prep+k_edge+k_photo", "_prep4": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group"}
     for suf, k in want.items():
         if name.endswith(suf):
             assert g.step_kernels() == k, name

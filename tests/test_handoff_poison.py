@@ -1,0 +1,78 @@
+"""Inter-workgroup hand-offs under load, poisoned.
+
+Every buffer the step hands between workgroups -- inside one launch (k_linearize's per-photo
+contributions and group sums, k_schur's item sums and the packed system: write-through `sc1`
+stores, one ticket add per workgroup, `sc1` loads by the last arriver) or between its kernels
+(erec / echain / eh, the Schur pair slots) -- is filled with NaN before every step
+(MCC_POISON_HANDOFF=1).  A consumer that read a word before its producer's store of this step
+landed would read the NaN, and the NaN would reach the parameters.  The runs are the full-size
+BASELINE rigs, where k_linearize and k_schur run several workgroups per CU (the condition the
+guide's measured row of the sc1 form does not cover), so the hand-offs are exercised under
+uneven, multi-workgroup-per-CU load.  Bar: the poisoned run's parameters are finite and bitwise
+equal to the clean run's, every step."""
+import os
+
+import numpy as np
+import pytest
+
+from multi_camera_calibration_amd import api, rig
+
+pytestmark = pytest.mark.gpu
+
+
+def run(p, poison, env, steps):   # poison: 0 off, 1 the hand-off buffers, 2 also dg (control)
+    old = {k: os.environ.get(k) for k in list(env) + ["MCC_POISON_HANDOFF"]}
+    os.environ.update(env)
+    os.environ["MCC_POISON_HANDOFF"] = str(int(poison))
+    try:
+        ba = api.BundleAdjuster(p)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    xs = []
+    for it in (1, 3, steps):   # COUNT criterion: exactly `it` Gauss-Newton steps from x0
+        x, _, n, _ = ba.optimize_extrinsics(p.x0, crit_type=api.MCC_CRIT_COUNT, max_count=it)
+        assert n == it or poison > 1
+        xs.append(x)
+    # the graph-launched throughput path too
+    ba.set_params(p.x0)
+    ba.step(steps)
+    ba.synchronize()
+    if poison < 2:
+        ba.check()
+    xs.append(ba.get_params())
+    out = xs
+    path = ba.step_kernels()
+    ba.close()
+    return np.stack(out), path
+
+
+@pytest.mark.parametrize("cfg,env,want", [
+    ("config2", {}, "k_linearize"),                    # fused: 500 photos, 2 per CU, two ticket levels
+    ("config4", {}, "k_group"),                        # k_group -> k_schur (items, blocks, solve)
+    ("config5", {}, "k_prep+k_edge+k_photo"),          # three-kernel split step, m = 42
+    ("config3", {}, "k_prep+k_edge+k_photo"),          # m = 90: k_schur -> k_solve
+    ("config5", {"MCC_GROUP": "1"}, "k_group"),        # k_group at 999 groups (4 per CU)
+])
+def test_poisoned_handoffs_bitwise(cfg, env, want):
+    p = rig.make_config(cfg)
+    steps = 6
+    clean, path = run(p, False, env, steps)
+    assert path == want
+    pois, _ = run(p, True, env, steps)
+    assert np.isfinite(pois).all()
+    assert np.array_equal(clean.view(np.uint32), pois.view(np.uint32))
+
+
+def test_poison_control_reaches_the_parameters():
+    """The mechanism's negative control: poisoning dg, which the step does read before writing it
+    (the previous solve's camera delta for the pending photo update), must show up."""
+    p = rig.make_config("config4", n_views=200)
+    try:
+        pois, _ = run(p, 2, {"MCC_FUSED": "0"}, 3)
+    except api.MccError:
+        return   # a NaN system reported not positive definite is a detection too
+    assert not np.isfinite(pois[1:]).all()
