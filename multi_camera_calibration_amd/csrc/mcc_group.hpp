@@ -288,6 +288,9 @@ __device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, i
     }
 }
 
+#ifndef MCC_GROUP_PAIR_THREADS
+#define MCC_GROUP_PAIR_THREADS 256   // threads the pair tasks may spread over (config4, 32 lanes: 256 29.0 vs 512 29.8 us per step)
+#endif
 #ifndef MCC_GROUP_OCC
 #define MCC_GROUP_OCC 2   // k_group workgroups per CU the register budget allows (LDS: ~64 KB each)
 #endif
@@ -740,7 +743,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     SSTAMP(stp, 9, 0);
     // the group's Schur pair products per camera-pair block -> its slot (k_photo's pair tasks)
     int H = 1;
-    while (H < 32 && 6 * nq * 2 * H <= NT) H *= 2;
+    while (H < 32 && 6 * nq * 2 * H <= (NT < MCC_GROUP_PAIR_THREADS ? NT : MCC_GROUP_PAIR_THREADS)) H *= 2;
     for (int t = tid; t < 6 * nq * H; t += NT) {
         const int h = t % H, k = t / H / 6, i0 = (t / H) % 6;
         const int4 pqv = spq[k];   // {first contribution, count, diagonal block << 1, slot offset}

@@ -2364,7 +2364,7 @@ __device__ __forceinline__ double bcast_group(double x) {
     return (GK & 2) ? e : d;
 }
 #ifndef MCC_GJB_SWAP
-#define MCC_GJB_SWAP 1   // 0: the pivot column by ds_bpermute and the pivot by v_readlane (A/B)
+#define MCC_GJB_SWAP 0   // 1: the pivot column by permlane16/32 swaps, the pivot by DPP (m = 90: 19.2 vs 18.7 us, slower)
 #endif
 template <int K>
 struct GjbStep {
