@@ -21,6 +21,9 @@
 // The per-corner and per-edge blocks are at most 6x6: FP64 VALU, latency
 // bound; MFMA appears only in the large-m reduced solve.  All reductions are fixed-order, so a run
 // is bitwise reproducible.
+#include <array>
+#include <map>
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -2363,6 +2366,9 @@ __device__ __forceinline__ double bcast_group(double x) {
     pl32_swap(d, e);                      // d(i, g) = c(i, g & 1), e(i, g) = c(i, 2 | (g & 1))
     return (GK & 2) ? e : d;
 }
+#ifndef MCC_GJB_IDLE4
+#define MCC_GJB_IDLE4 0
+#endif
 #ifndef MCC_GJB_SWAP
 #define MCC_GJB_SWAP 0   // 1: the pivot column by permlane16/32 swaps, the pivot by DPP (m = 90: 19.2 vs 18.7 us, slower)
 #endif
@@ -2400,10 +2406,61 @@ template <>
 struct GjbStep<16> {
     __device__ __forceinline__ static void run(double (&)[4], int, bool&) {}
 };
+// Two pivots per step (K even: columns K, K + 1 share a lane's column group): the 2 x 2 pivot block
+// P = [[a, b], [c, d]] inverted in closed form, Q = P^-1 (one reciprocal of det), then
+// rows i outside {K, K+1}: A[i][j] -= [A[i][K] A[i][K+1]] Q [A[K][j]; A[K+1][j]], columns K, K+1 <-
+// -[A[i][K] A[i][K+1]] Q; the pivot rows <- Q times them; the pivot block <- Q.  The same result as
+// two single pivots in exact arithmetic (SPD: a > 0 and det = a d' > 0), with about 3/4 of their
+// instructions (one reciprocal chain, one set of multipliers).
+#ifndef MCC_GJB_PAIR
+#define MCC_GJB_PAIR 0   // 1: pairs of pivots (m = 90: 18.72 vs 18.63 us per solve, m = 126: 28.4 vs 29.8)
+#endif
+template <int K>
+struct GjbPair {
+    __device__ __forceinline__ static void run(double (&v)[4], int lane, bool& ok) {
+        constexpr int gk = K >> 2, c0 = K & 3, c1 = c0 + 1;
+        const int i = lane & 15, g = lane >> 4;
+        const double a = readlane_f64(v[c0], K + 16 * gk), b = readlane_f64(v[c1], K + 16 * gk);
+        const double c = readlane_f64(v[c0], K + 1 + 16 * gk), d = readlane_f64(v[c1], K + 1 + 16 * gk);
+        const double r0 = __shfl(v[c0], i + 16 * gk), r1 = __shfl(v[c1], i + 16 * gk);   // A[i][K], A[i][K+1]
+        const double det = fma(a, d, -(b * c));
+        ok &= a > 0.0 && det > 0.0;
+        const double pd = det > 0.0 ? det : 1.0;
+        double id = __builtin_amdgcn_rcp(pd);
+        id = fma(id, fma(-pd, id, 1.0), id);
+        const double q00 = d * id, q01 = -b * id, q10 = -c * id, q11 = a * id;
+        const bool p0 = i == K, p1 = i == K + 1;
+        double m0 = fma(r0, q00, r1 * q10), m1 = fma(r0, q01, r1 * q11);
+        m0 = p0 ? -q00 : (p1 ? -q10 : m0);
+        m1 = p0 ? -q01 : (p1 ? -q11 : m1);
+        const double keep = (p0 || p1) ? 0.0 : 1.0;
+        double pa[4], pb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pa[q] = gjb_bcast16<K>(v[q]);
+            pb[q] = gjb_bcast16<K + 1>(v[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fma(-m1, pb[q], fma(-m0, pa[q], v[q] * keep));
+        if (g == gk) {
+            v[c0] = p0 ? q00 : (p1 ? q10 : -m0);
+            v[c1] = p0 ? q01 : (p1 ? q11 : -m1);
+        }
+        GjbPair<K + 2>::run(v, lane, ok);
+    }
+};
+template <>
+struct GjbPair<16> {
+    __device__ __forceinline__ static void run(double (&)[4], int, bool&) {}
+};
 __device__ __forceinline__ bool gjb_inverse16_regs(double (&v)[4], double* PV, int lane) {
     const int i = lane & 15, g = lane >> 4;
     bool ok = true;
+#if MCC_GJB_PAIR
+    GjbPair<0>::run(v, lane, ok);
+#else
     GjbStep<0>::run(v, lane, ok);
+#endif
 #pragma unroll
     for (int c = 0; c < 4; ++c) PV[i * kBlkLd + 4 * g + c] = v[c];
     return ok;
@@ -2529,10 +2586,22 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
                 for (int it = wave; it <= n3; it += nw) item(it);
             } else if (wave == 0) {
                 item(it0);
+                if (gst && tid == 0) gst[40 + kb] = (long long)__builtin_amdgcn_s_memtime();
                 const int kn = kb + 1;
                 bad |= !gjb_inverse16(A + 16 * kn * ld + 16 * kn, ld, PV + (kn & 1) * 16 * kBlkLd, lane);
+                if (gst && tid == 0) gst[48 + kb] = (long long)__builtin_amdgcn_s_memtime();
             } else {
+#if MCC_GJB_IDLE4
+                // wave 4 shares wave 0's SIMD: it sits out, so the pivot chain has the SIMD alone
+                if (nw > 5 && wave == 4) {
+                } else {
+                    const int wid = nw > 5 && wave > 4 ? wave - 2 : wave - 1, nwk = nw > 5 ? nw - 2 : nw - 1;
+                    for (int q = wid; q < n3; q += nwk) item(q < it0 ? q : q + 1);
+                }
+#else
                 for (int q = wave - 1; q < n3; q += nw - 1) item(q < it0 ? q : q + 1);   // n3 - 1 blocks + rhs
+#endif
+                if (gst && tid == 64) gst[56 + kb] = (long long)__builtin_amdgcn_s_memtime();
             }
         }
         __syncthreads();
@@ -3150,13 +3219,26 @@ static hipError_t set_group_attrs(size_t group_shmem) {
     return err;
 }
 
+// The dynamic-LDS limits only ever grow within a process (per device): a graph captured for an
+// earlier, larger problem keeps launching with the LDS it was captured with after a smaller problem
+// is created.
 hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem) {
     hipError_t err = hipSuccess;
+    static std::mutex mu;
+    static std::map<int, std::array<size_t, 4>> high;   // device -> {group, linearize, photo, solve}
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    auto& hw = high[dev];
+    size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, max_cpp), ss = mcc_solve_shmem(m);
+    group_shmem = hw[0] = std::max(hw[0], group_shmem);
+    shmem = hw[1] = std::max(hw[1], shmem);
+    photo_shmem = hw[2] = std::max(hw[2], photo_shmem);
+    ss = hw[3] = std::max(hw[3], ss);
     if (group_shmem > 64 * 1024) {
         for (hipError_t e : {set_group_attrs<16>(group_shmem), set_group_attrs<32>(group_shmem)})
             if (e != hipSuccess) err = e;
     }
-    const size_t shmem = mcc_lin_shmem(max_epp, n_cams, m, max_cpp);
     if (shmem > 64 * 1024) {
 #define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
         for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
@@ -3169,7 +3251,6 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, siz
         hipError_t e = hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)photo_shmem);
         if (e != hipSuccess) err = e;
     }
-    const size_t ss = mcc_solve_shmem(m);
     if (ss > 60 * 1024) {
         hipError_t e1 = hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
         hipError_t e2 = hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);

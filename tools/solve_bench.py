@@ -19,6 +19,10 @@ for m in ms:
     row = []
     for kb in range(nb):
         a, b, c = st[1 + 3 * kb] - t0, st[2 + 3 * kb] - t0, st[3 + 3 * kb] - t0
-        row.append(f"kb{kb}: start {a} scaled {b} elim {c}")
+        extra = ""
+        if kb + 1 < nb and st[40 + kb]:
+            extra = (f"  [w0 item done {st[40 + kb] - t0}, inverse done {st[48 + kb] - t0}; "
+                     f"w1 items done {st[56 + kb] - t0}]")
+        row.append(f"kb{kb}: start {a} scaled {b} elim {c}{extra}")
     print("   " + "\n   ".join(row))
     print(f"   end {st[63] - t0}")
