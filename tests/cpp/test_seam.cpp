@@ -278,7 +278,9 @@ static void fill(MC& mc, const Blob& b) {
         mc._edgeList.emplace_back(c, b.C + b.ephoto[e], pi, mcc::multicalib::eye4());
         mc._edgeList.back().patternSide = b.eside[e];
     }
-    mc.mcc::multicalib::MultiCameraCalibration::paras2vertex(b.x0);
+    // the host layer's paras2vertex(vector) by virtual dispatch: DoubleSide's layout is [ds | photos]
+    // (a qualified call would run the base class's [cameras | photos] on every model)
+    static_cast<mcc::multicalib::MultiCameraCalibration&>(mc).paras2vertex(b.x0);
 }
 
 static long long ulp_diff(float a, float b) {
@@ -293,8 +295,19 @@ template <class Lib, class Sub>
 static int compare(const Blob& b, Lib& lib, Sub& sub) {
     fill(lib, b);
     fill(sub, b);
-    const double e_lib = lib.optimizeExtrinsics();   // the device loop (the library's own class)
-    const double e_sub = sub.optimizeExtrinsics();   // the reference's host loop through the overrides
+    double e_lib = 0.0, e_sub = 0.0;
+    try {
+        e_lib = lib.optimizeExtrinsics();   // the device loop (the library's own class)
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "library class: %s\n", e.what());
+        throw;
+    }
+    try {
+        e_sub = sub.optimizeExtrinsics();   // the reference's host loop through the overrides
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "subclass, after %d linearisations: %s\n", sub.calls.jac, e.what());
+        throw;
+    }
     const std::vector<float> x_lib = lib.buildParaVector(), x_sub = sub.buildParaVector();
     long long worst = 0;
     for (size_t i = 0; i < x_lib.size(); ++i) worst = std::max(worst, ulp_diff(x_lib[i], x_sub[i]));

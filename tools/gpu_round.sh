@@ -5,7 +5,7 @@
 #   3. rocprofv3 --kernel-trace --stats of the driver-settings bench, one process per config
 # Usage: tools/gpu_round.sh <tag> [tests|bench|prof ...]   (default: all three)
 set -o pipefail
-TAG=${1:-r02}
+TAG=${1:-r03}
 shift
 STEPS=${*:-tests bench prof}
 R=$PWD
@@ -33,15 +33,11 @@ for s in $STEPS; do
         echo "bench (defaults):"; cut -c1-400 "$OUT/bench_default.json"
         ;;
     prof)
-        # one process per config (--no-extra), and config4 with eager launches (MCC_GRAPH=0): under
-        # rocprofv3 --kernel-trace, graph-launched split steps abort in two reproducible cases --
-        # HSA_STATUS_ERROR_INVALID_PACKET_FORMAT when they follow the fused step's graphs in the
-        # same process (config2 then config3), and a host SIGSEGV inside hipGraphLaunch for the
-        # m = 18 split step (config4; config2 with MCC_FUSED=0).  Eager launches, m = 6 / 90 split
-        # steps alone, and every run without the profiler are fine (tools/repro_prof.sh).
-        for cfg in config2 config3 config4 config5; do
-            g=1; [ $cfg = config4 ] && g=0
-            ( cd /tmp && export TMPDIR=/tmp && export MCC_GRAPH=$g && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run \
+        # one process per config (--no-extra), graph-launched, with HIP's graph packet capture off:
+        # with it on, rocprofv3's kernel-trace interception crashes intermittently inside
+        # hipGraphLaunch; tools/profile_r03.sh adds the PMC passes
+        for cfg in config4 config2 config3 config5; do
+            ( cd /tmp && export TMPDIR=/tmp && export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats_$cfg" -o run \
                 --output-format csv -- python3 "$R/bench.py" --config $cfg --steps 20 --warmup 5 --no-cpu --no-parity --no-extra \
                 > "$OUT/prof_$cfg.json" 2> "$OUT/prof_$cfg.err" ) || exit 13
             f=$(find "$OUT/stats_$cfg" -name "*kernel_stats.csv" | head -n 1)
