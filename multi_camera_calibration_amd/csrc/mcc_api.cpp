@@ -172,6 +172,7 @@ struct mcc_problem {
     // read of a word its producer has not yet stored this step shows up in the result
     bool poison = false;
     int poison_level = 0;
+    bool peer_push = true;   // m > 30 with the peer transport: k_peer_push sends from many workgroups
     int n_prep = 0, prep_lanes = 1;   // MCC_PREP_LANES=4: k_prep4 (measured slower at configs 3 and 5)
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
@@ -313,7 +314,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
                 HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used + 1], p->stream));
                 p->ev_x_used += 2;
             }
-            SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false)};
+            SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false), 0};
             HIPCHK(mcc_launch_solve(so, p->stream));
         }
         if (tim) {
@@ -353,7 +354,11 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
         }
     }
     if (split) {
-        SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer)};
+        SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer), 0};
+        if (peer && p->peer_push) {   // MCC_PEER_PUSH=0: k_solve's one workgroup sends too
+            HIPCHK(mcc_launch_peer_push(so.peer, p->state.p, p->packed.p, p->stream));
+            so.pushed = 1;
+        }
         HIPCHK(mcc_launch_solve(so, p->stream));
     }
     if (tim) {
@@ -611,6 +616,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
     if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);
     if (const char* f = std::getenv("MCC_GROUP_LANES")) p->group_lanes = std::atoi(f) == 16 ? 16 : 32;
+    if (const char* f = std::getenv("MCC_PEER_PUSH")) p->peer_push = std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_POISON_HANDOFF")) {
         p->poison_level = std::atoi(f);
         p->poison = p->poison_level != 0;

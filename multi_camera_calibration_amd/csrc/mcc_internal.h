@@ -215,6 +215,7 @@ struct SolveArgs {
     SolveCtx ctx;
     double* packed;
     PeerCtx peer;            // nranks > 0: exchange the packed system with the peers first
+    int pushed;              // k_peer_push already sent this rank's system (k_solve only receives)
 };
 
 struct BacksubArgs {
@@ -254,6 +255,7 @@ hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, boo
 hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
+hipError_t mcc_launch_peer_push(const mcc::PeerCtx& pc, const mcc::State* st, const double* vals, hipStream_t s);
 hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
 hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);

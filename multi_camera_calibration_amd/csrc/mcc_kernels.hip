@@ -848,7 +848,7 @@ __device__ __forceinline__ double peer_sum(const PeerCtx& pc, unsigned ep, int t
 // The exchange of the packed system held in vals[0, Lc) (global, this workgroup's own copy):
 // every thread sends its entries, then replaces them with the rank-ordered sums.  Returns false
 // (state error bit 2, done) when a peer did not deliver within the timeout.  Whole workgroup.
-__device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, double* vals) {
+__device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, double* vals, bool send = true) {
     __shared__ unsigned ep_s;
     __shared__ int to_s;
     const int tid = threadIdx.x;
@@ -859,7 +859,8 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
     }
     __syncthreads();
     const unsigned ep = ep_s;
-    for (int t = tid; t < pc.Lc; t += blockDim.x) peer_send(pc, ep, t, vals[t]);
+    if (send)
+        for (int t = tid; t < pc.Lc; t += blockDim.x) peer_send(pc, ep, t, vals[t]);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     bool timeout = false;
     for (int t = tid; t < pc.Lc; t += blockDim.x) vals[t] = peer_sum(pc, ep, t, vals[t], t0, timeout);
@@ -2846,7 +2847,7 @@ __global__ __launch_bounds__(1024) void k_solve(SolveArgs a) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;
     double* r = sm + m * m;
-    if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed)) return;
+    if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed, !a.pushed)) return;
     if (m > 30) {   // the blocked elimination reads the packed system directly (LDS: x, A, pivot inverse)
         solve_global<true>(a.ctx, a.packed, sm, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
         return;
@@ -2862,6 +2863,17 @@ __global__ __launch_bounds__(1024) void k_solve(SolveArgs a) {
     for (int t = tid; t < m; t += blockDim.x) r[t] = a.packed[ntri + t];
     __syncthreads();
     solve_global<false>(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+}
+
+// This rank's packed system -> every peer's inbox from many workgroups (the m > 30 split step, in
+// front of k_solve, which then only receives): 2 Lc LL words per peer -- 68 KB at m = 90, ~480 KB
+// per rank at 8 ranks -- are too many 8-B system-scope stores for one workgroup's store issue.
+// The epoch is read here and advanced only by k_solve's exchange after this kernel has ended.
+__global__ __launch_bounds__(256) void k_peer_push(PeerCtx pc, const State* st, const double* vals) {
+    if (st->done) return;
+    const unsigned ep = st->epoch + 1u;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < pc.Lc; t += gridDim.x * blockDim.x)
+        peer_send(pc, ep, t, vals[t]);
 }
 
 // ---------------------------------------------------------------- mcc_debug_solve
@@ -3271,6 +3283,13 @@ hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
     // m > 30: 8 waves, so the block eliminations of a pivot step (up to (nb - 1)^2 16 x 16 MFMA
     // products) are not what waits on the next pivot inverse
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(a.ctx.m > 30 ? kSolveThreads : 256), mcc_solve_shmem(a.ctx.m), s, a);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_peer_push(const PeerCtx& pc, const State* st, const double* vals, hipStream_t s) {
+    // ~16 KB of words per workgroup: 8 ranks at m = 90 -> 30 workgroups
+    const long long bytes = 16LL * pc.Lc * (pc.nranks - 1);
+    const int grid = (int)std::min<long long>(64, std::max<long long>(1, (bytes + 16383) / 16384));
+    hipLaunchKernelGGL(k_peer_push, dim3(grid), dim3(256), 0, s, pc, st, vals);
     return hipGetLastError();
 }
 hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s) {
