@@ -211,6 +211,7 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
         m = measure(ba, steps, warmup, 0.15, max(100, steps))
         st = ba.stats()
         kern = lin_kernels(ba)
+        solve = ba.solve_stats()
     finally:
         ba.close()
     ms = m["dt"] / steps * 1e3
@@ -220,6 +221,10 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
            "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
            "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=kern),
            "rig_generation_s": round(gen_s, 2)}
+    if solve["warm"] or solve["direct"]:
+        # m > 30: solves by refinement with the previous step's inverse (k_sinv, side stream) over
+        # every step of this process (ramp, warmup, timed, window), and how many fell back
+        out["warm_solve"] = solve
     fp = load_profile("fp64", name, p.n_photos)
     if fp and fp.get("fp64_flops_per_launch"):
         tf = fp["fp64_flops_per_launch"] / (m["lin_ms"] * 1e-3) / 1e12
@@ -251,6 +256,7 @@ def strong_line(name: str, rank: int, world: int, local_rank: int, same_device: 
             out[tr] = {"value": full.n_corners / (ms * 1e-3), "ms_per_step": ms,
                        "kernel_ms_per_launch": m["lin_ms"], "step_ms_events": m["step_ms_ev"],
                        "exchange_ms": m["xchg_ms"], "exchanges_timed": m["n_xchg"]}
+        out["warm_solve"] = ba.solve_stats()
     finally:
         ba.close()
     best = min((t for t in ("peer", "rccl") if t in out), key=lambda t: out[t]["ms_per_step"])
@@ -336,6 +342,7 @@ def main():
     m = measure(ba, args.steps, args.warmup, args.ramp_seconds, max(100, args.steps))
     st = ba.stats()
     kern = lin_kernels(ba)
+    solve = ba.solve_stats()
     corners_total = float(full.n_corners)
     value = corners_total * args.steps / m["dt"]
     ms_per_step = m["dt"] / args.steps * 1e3
@@ -389,6 +396,8 @@ def main():
                             "flops_per_corner": fp["fp64_flops_per_corner"],
                             "source": "profiles/fp64_*.json (rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, "
                                       "an upper bound) / the event-timed launch"}
+    if solve["warm"] or solve["direct"]:
+        out["warm_solve"] = solve
     if strong:
         out["strong"] = strong
     if not args.no_parity and world == 1:

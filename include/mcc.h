@@ -157,6 +157,13 @@ int mcc_peer_init(mcc_problem *p, const unsigned char *handles /* [64 * nranks],
 int mcc_peer_enable(mcc_problem *p, int on);
 
 /* ---- diagnostics / measurement */
+/* the m > 30 split step's warm solves since mcc_create (k_solve refines with the previous step's
+ * inverse, which a resident helper kernel computes while the step linearises): out[5] = {solves by
+ * refinement, refinement corrections in them, refinements that did not converge (the direct
+ * elimination ran instead), direct solves for want of an inverse (a run's first step), direct
+ * solves because the helper was late}; all zero when the problem takes the direct elimination only
+ * (m <= 30, m > 96, MCC_WARM=0) */
+int mcc_solve_stats(mcc_problem *p, long long *out);
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
 /* test / measurement: the m > 30 dense solve alone (k_solve's elimination), x = S^-1 r for a

@@ -112,6 +112,7 @@ def lib():
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_timing_exchange.argtypes = [ctypes.c_void_p, _f64p, _i32p]
         L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
+        L.mcc_solve_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
         L.mcc_problem_path.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
         L.mcc_comm_unique_id.argtypes = [ctypes.c_char_p]
         L.mcc_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
@@ -334,6 +335,15 @@ class BundleAdjuster:
         v = [ctypes.c_longlong(0) for _ in range(4)]
         _check(lib().mcc_problem_stats(self.h, *[ctypes.byref(t) for t in v]), "mcc_problem_stats")
         return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
+
+    def solve_stats(self):
+        """The m > 30 warm solves (mcc_solve_stats): solves by refinement with the previous step's
+        inverse, their refinement corrections, refinements that fell back to the direct elimination,
+        direct solves for want of an inverse, direct solves because the helper was late (all zero on
+        the direct-only paths)."""
+        v = (ctypes.c_longlong * 5)()
+        _check(lib().mcc_solve_stats(self.h, v), "mcc_solve_stats")
+        return dict(warm=v[0], corrections=v[1], fallbacks=v[2], direct=v[3], late=v[4])
 
     def path(self):
         """'fused' (one kernel per step) or 'split' (k_prep, k_edge, k_photo, k_schur, k_solve)."""

@@ -174,6 +174,15 @@ struct mcc_problem {
     int poison_level = 0;
     bool peer_push = true;   // m > 30 with the peer transport: k_peer_push sends from many workgroups
     int n_prep = 0, prep_lanes = 1;   // MCC_PREP_LANES=4: k_prep4 (measured slower at configs 3 and 5)
+    // warm solve (m > 30 split step, MCC_WARM=0 turns it off): a resident helper kernel on a side
+    // stream (one per batch of update steps) inverts each step's reduced system while the next step
+    // linearises; the next k_solve refines with it (WarmCtx, mcc_internal.h)
+    bool warm = false;
+    hipStream_t side = nullptr;      // the helper's stream
+    double* sinv = nullptr;          // [M x M] (ordinary memory)
+    double* sprev = nullptr;         // uncached: packed [S | r]
+    unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
+    DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
@@ -228,6 +237,10 @@ namespace {
 
 mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
     return mcc::SolveCtx{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+}
+
+mcc::WarmCtx warm_ctx(mcc_problem* p) {
+    return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->sprev, p->wsync, p->warm_stats.p};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
@@ -314,7 +327,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
                 HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used + 1], p->stream));
                 p->ev_x_used += 2;
             }
-            SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false), 0};
+            SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, false), 0, {}};
             HIPCHK(mcc_launch_solve(so, p->stream));
         }
         if (tim) {
@@ -354,7 +367,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
         }
     }
     if (split) {
-        SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer), 0};
+        SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer), 0, {}};
+        if (p->warm && do_update) so.warm = warm_ctx(p);
         if (peer && p->peer_push) {   // MCC_PEER_PUSH=0: k_solve's one workgroup sends too
             HIPCHK(mcc_launch_peer_push(so.peer, p->state.p, p->packed.p, p->stream));
             so.pushed = 1;
@@ -392,6 +406,11 @@ int build_graph(mcc_problem* p, int k) {
 }
 int launch_update_steps(mcc_problem* p, int n) {
     if (p->timing_window) p->win_steps += n;
+    if (p->warm && n > 0) {
+        // the batch's helper: after the previous one (side-stream order), with the stop flag cleared
+        HIPCHK(hipMemsetAsync(p->wsync + 2, 0, sizeof(unsigned), p->side));
+        HIPCHK(mcc_launch_sinv_helper(warm_ctx(p), p->m, n, p->side));
+    }
     if (p->timing || !p->use_graph) {
         for (int i = 0; i < n; ++i) {
             int rc = enqueue_step(p, 1, nullptr);
@@ -845,6 +864,19 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (!p->fused && p->use_group && p->group_shmem > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many edges / Schur pairs of one photo group for k_group's LDS"));
     HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->use_group ? p->group_shmem : 0));
+    p->warm = !p->fused && p->m > 30;
+    if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
+    p->warm = p->warm && p->m <= 96;   // the staged system and inverse fit k_solve's LDS up to M = 96
+    if (p->warm) {
+        const size_t M = 16 * (size_t)((p->m + 15) / 16);
+        HIPC(hipMalloc((void**)&p->sinv, M * M * sizeof(double)));   // cached: the helper releases it, k_solve reads it in a later launch
+        HIPC(hipExtMallocWithFlags((void**)&p->sprev, ((size_t)p->ntri + p->m + 2) * sizeof(double), hipDeviceMallocUncached));
+        HIPC(hipExtMallocWithFlags((void**)&p->wsync, 4 * sizeof(unsigned), hipDeviceMallocUncached));
+        HIPC(hipMemset(p->wsync, 0, 4 * sizeof(unsigned)));
+        HIPC(p->warm_stats.alloc(5));
+        HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
+        HIPC(stream_pool().take(d->device, &p->side));
+    }
 #undef HIPC
     (void)rc;
     *out = p;
@@ -854,7 +886,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
 void mcc_destroy(mcc_problem* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
+    const bool side_drained = p->side && hipStreamSynchronize(p->side) == hipSuccess;
     const bool drained = p->stream && hipStreamSynchronize(p->stream) == hipSuccess;
+    if (p->sinv) (void)hipFree(p->sinv);
+    if (p->sprev) (void)hipFree(p->sprev);
+    if (p->wsync) (void)hipFree(p->wsync);
+    p->warm_stats.release();
     for (auto& g : p->gexec)
         if (g) (void)hipGraphExecDestroy(g);
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
@@ -882,6 +919,8 @@ void mcc_destroy(mcc_problem* p) {
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused
     else if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (side_drained) stream_pool().give(p->device, p->side);
+    else if (p->side) (void)hipStreamDestroy(p->side);
     delete p;
 }
 
@@ -1058,6 +1097,17 @@ int mcc_debug_solve(int device, int m, const double* packed, double* x, int reps
         *us_per_solve = 1e3 * (double)ms / reps;
     }
     return err ? fail(MCC_ENOTPD, "mcc_debug_solve: not positive definite") : MCC_OK;
+}
+
+int mcc_solve_stats(mcc_problem* p, long long* out) {
+    if (!p || !out) return fail(MCC_EINVAL, "null argument");
+    HIPCHK(hipSetDevice(p->device));
+    std::memset(out, 0, 5 * sizeof(long long));
+    if (!p->warm) return MCC_OK;
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipStreamSynchronize(p->side));
+    HIPCHK(hipMemcpy(out, p->warm_stats.p, 5 * sizeof(long long), hipMemcpyDeviceToHost));
+    return MCC_OK;
 }
 
 int mcc_debug_residuals(mcc_problem* p, const float* x, float* res) {

@@ -211,11 +211,28 @@ struct SchurArgs {
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
 };
 
+// The m > 30 solve with the previous step's inverse (the "warm" solve, solve_large in
+// mcc_kernels.hip): a resident helper kernel on a side stream (k_sinv_helper) inverts each update
+// step's reduced system while the next step linearises; the next k_solve solves its own system by
+// iterative refinement preconditioned with that inverse and falls back to the direct elimination
+// when the refinement does not converge within kWarmMaxIters corrections.  sinv_ok_sys, sprev and
+// sync are uncached device memory (the helper and the k_solve launches hand them over while both
+// run); sinv is ordinary memory, written back by the helper (agent release) before its epoch.
+struct WarmCtx {
+    double* sinv;            // [M x M] (M = 16 ceil(m / 16), row-major) the helper's inverse
+    int* sinv_ok_sys;        // the helper's elimination found the system positive definite
+    double* sprev;           // [packed [S | r] rounded up to even] the last solved system, for the helper
+    unsigned* sync;          // [3] epochs: systems published by k_solve, systems inverted by the helper; stop
+    long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), helper late
+};
+constexpr int kWarmMaxIters = 8;
+
 struct SolveArgs {
     SolveCtx ctx;
     double* packed;
     PeerCtx peer;            // nranks > 0: exchange the packed system with the peers first
     int pushed;              // k_peer_push already sent this rank's system (k_solve only receives)
+    WarmCtx warm;            // m > 30: sync == null -> the direct elimination
 };
 
 struct BacksubArgs {
@@ -257,6 +274,7 @@ hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
 hipError_t mcc_launch_peer_push(const mcc::PeerCtx& pc, const mcc::State* st, const double* vals, hipStream_t s);
 hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s);
+hipError_t mcc_launch_sinv_helper(const mcc::WarmCtx& w, int m, int n_systems, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
 hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);
 hipError_t mcc_launch_peer_max(const mcc::PeerCtx& pc, mcc::State* st, double* v, hipStream_t s);

@@ -878,7 +878,8 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
 }
 
 template <bool LARGE>
-__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2);
+__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
+                                             const WarmCtx* warm = nullptr);
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
@@ -2268,7 +2269,7 @@ __device__ __forceinline__ double sub_sum(double v, int tpr) {
 // its column-k entry.  S is SPD: no pivoting.  Writes delta_i = r_i / S_ii into r[].
 
 template <int MM>
-__device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int lane, int* err) {
+__device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int lane, int* err, int* bad_lds) {
     // every load address is in range for every lane: lanes >= m read row 0 and stay idle
     const int li = lane < m ? lane : 0;
     double row[MM];
@@ -2301,6 +2302,7 @@ __device__ __forceinline__ void gj_rows(const double* S, double* r, int m, int l
         rr -= f * pr[MM];
     }
     if (bad && lane == 0) atomicOr(err, 2);
+    if (bad_lds && lane == 0) *bad_lds = bad ? 1 : 0;   // every call writes it (no initialisation race)
     if (lane < m) r[lane] = rr / dii;
 }
 
@@ -2477,7 +2479,7 @@ __device__ __forceinline__ bool gjb_inverse16(const double* Pk, int ld, double* 
 // boundaries, slot 0 after the loads, 1 + 3 kb .. 3 + 3 kb per pivot block step
 #define GJB_STAMP(k) do { if (gst && threadIdx.x == 0) gst[k] = (long long)__builtin_amdgcn_s_memtime(); } while (0)
 __device__ __forceinline__ void gj_blocked(const double* packed, double* x, double* A, double* PV, int m, int* err,
-                                           long long* gst) {
+                                           long long* gst, int* bad_lds = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
     const int nb = (m + 15) / 16, M = 16 * nb, ld = M + 1, ntri = m * (m + 1) / 2;
     // rhs, padding and the packed triangle: every global load is issued before the first LDS store
@@ -2608,12 +2610,408 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
         __syncthreads();
         GJB_STAMP(3 + 3 * kb);
     }
-    if (bad && lane == 0) atomicOr(err, 2);
+    if (bad && lane == 0) {
+        atomicOr(err, 2);
+        if (bad_lds) *bad_lds = 1;
+    }
 }
 
-__device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err) {
+// ---------------------------------------------------------------- warm solve (m > 30, k_solve)
+// S_{t+1} x = r by iterative refinement with the inverse of the previous step's system, which the
+// resident helper k_sinv_helper computed while this step linearised:
+//   x_0 = S_t^-1 r,  x_{k+1} = x_k + S_t^-1 (r - S_{t+1} x_k).
+// Hand-off with the helper through uncached memory (every access goes to HBM, so no cache holds a
+// stale copy): k_solve publishes S_t (sprev, then sync[0] = t's epoch, after its stores drained);
+// the helper inverts it into sinv and publishes sync[1] = that epoch; the next k_solve waits for
+// sync[1] == sync[0] before it reads sinv or overwrites sprev.  It always refines with exactly the
+// previous step's inverse, so the result does not depend on timing.
+// Thread t holds row i = t >> 2 of S_{t+1} and of S_t^-1, columns [24 g, 24 g + 24) (g = t & 3; zero
+// beyond m), in registers; a product A v is the quad's four partial dot products (v from LDS, six
+// 16-B reads in flight) added by two DPP quad permutes.  (Measured, not kept: 4 x 6 blocks per
+// thread with a 16-lane butterfly per row -- 4x less LDS traffic per product, but ~5.6k instead of
+// ~3.3k cycles per correction.)
+// Converged when every equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i
+// (tested before each correction, so a preconditioner as good as the systems' step-to-step change
+// costs none); otherwise (kWarmMaxIters corrections, a NaN) the direct elimination runs.
+constexpr int kWarmQ = 24;                 // M <= 96 (m <= 96): the staged S and S^-1 fit in LDS
+constexpr int kWarmN = 4 * kWarmQ;
+constexpr long long kWarmWaitTicks = 50000;        // k_solve waits <= 0.5 ms for the helper (100 MHz ticks)
+constexpr long long kHelperIdleTicks = 2000000;    // the helper exits after 20 ms without a new system
+__device__ __forceinline__ double wave_max(double v) {
+    {
+        double a = v, b = v;
+        pl32_swap(a, b);
+        v = fmax(a, b);
+    }
+    {
+        double a = v, b = v;
+        pl16_swap(a, b);
+        v = fmax(a, b);
+    }
+    v = fmax(v, dpp_f64<kDppRor8>(v));
+    v = fmax(v, dpp_f64<kDppRor4>(v));
+    v = fmax(v, dpp_f64<kDppXor2>(v));
+    v = fmax(v, dpp_f64<kDppXor1>(v));
+    return v;
+}
+// a workgroup barrier that orders LDS only (no wait for outstanding global stores)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+// the quad's dot product of row i with v over its chunk (no guards, so every 16-B LDS read is in
+// flight at once), summed over the quad
+__device__ __forceinline__ double warm_dot(const double (&a)[kWarmQ], const double* v) {
+    double2 w[kWarmQ / 2];
+#pragma unroll
+    for (int c = 0; c < kWarmQ / 2; ++c) w[c] = reinterpret_cast<const double2*>(v)[c];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+    for (int c = 0; c < kWarmQ / 2; c += 2) {
+        s0 = fma(a[2 * c], w[c].x, s0);
+        s1 = fma(a[2 * c + 1], w[c].y, s1);
+        s2 = fma(a[2 * c + 2], w[c + 1].x, s2);
+        s3 = fma(a[2 * c + 3], w[c + 1].y, s3);
+    }
+    double s = (s0 + s1) + (s2 + s3);
+    s += dpp_f64<kDppXor1>(s);
+    s += dpp_f64<kDppXor2>(s);
+    return s;
+}
+// the same for A v and |A| |v| together (the residual and its componentwise scale)
+__device__ __forceinline__ double warm_dot_abs(const double (&a)[kWarmQ], const double* v, double& sa) {
+    double2 w[kWarmQ / 2];
+#pragma unroll
+    for (int c = 0; c < kWarmQ / 2; ++c) w[c] = reinterpret_cast<const double2*>(v)[c];
+    double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < kWarmQ / 2; ++c) {
+        s0 = fma(a[2 * c], w[c].x, s0);
+        s1 = fma(a[2 * c + 1], w[c].y, s1);
+        t0 = fma(fabs(a[2 * c]), fabs(w[c].x), t0);
+        t1 = fma(fabs(a[2 * c + 1]), fabs(w[c].y), t1);
+    }
+    double s = s0 + s1, t = t0 + t1;
+    s += dpp_f64<kDppXor1>(s);
+    t += dpp_f64<kDppXor1>(t);
+    s += dpp_f64<kDppXor2>(s);
+    t += dpp_f64<kDppXor2>(t);
+    sa = t;
+    return s;
+}
+__device__ __forceinline__ int warm_lc2(int m) { return (m * (m + 1) / 2 + m + 1) / 2; }   // packed [S | r] in double2
+// LDS doubles of the warm path behind x (kWarmN): packed [S | r] (even length), S^-1 (M x (M + 2)),
+// the residual (kWarmN), wave maxima
+__host__ __device__ __forceinline__ size_t warm_shmem_doubles(int m) {
+    const int M = 16 * ((m + 15) / 16);
+    return 2 * (size_t)((m * (m + 1) / 2 + m + 1) / 2) + (size_t)M * (M + 2) + kWarmN + 48;
+}
+// row i's chunk of S_{t+1} from the staged packed upper triangle (zero beyond m)
+__device__ __forceinline__ void warm_gather_s(const double* Pk, int m, double (&Sr)[kWarmQ]) {
+    const int i = threadIdx.x >> 2, g = threadIdx.x & 3;
+    const bool row = i < m;
+    const int ic = row ? i : 0;
+#pragma unroll
+    for (int c = 0; c < kWarmQ; ++c) {
+        const int j = min(g * kWarmQ + c, m - 1);
+        const int lo = min(ic, j), hi = max(ic, j);
+        const double v = Pk[lo * m - lo * (lo - 1) / 2 + (hi - lo)];
+        Sr[c] = row && g * kWarmQ + c < m ? v : 0.0;
+    }
+}
+// the refinement: Sr (registers), Iv = S_t^-1 (LDS, M + 2 stride), Pk = packed [S | r] (LDS);
+// x[kWarmN] receives the solution (zero beyond m)
+__device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const double* Pk, double* x, double* work,
+                            int m, long long* stats) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int nw = kSolveThreads / 64;
+    const int i = tid >> 2, g = tid & 3;
+    constexpr int Qp = kWarmQ, nv = kWarmN;
+    const int ntri = m * (m + 1) / 2, M = 16 * ((m + 15) / 16);
+    const bool row = i < m;
+    const int ic = row ? i : 0;
+    double Ir[kWarmQ];
+#pragma unroll
+    for (int c = 0; c < kWarmQ; c += 2) {
+        const int j = g * Qp + c;
+        const double2 v = *reinterpret_cast<const double2*>(Iv + ic * (M + 2) + min(j, M - 2));
+        Ir[c] = row && j < m ? v.x : 0.0;
+        Ir[c + 1] = row && j + 1 < m ? v.y : 0.0;
+    }
+    const double rr = row ? Pk[ntri + i] : 0.0;
+    double* rv = work;            // [nv] right-hand side, then the residual
+    double* red = work + nv;      // [nw] per-wave max of the scaled residual
+    if (g == 0 && i < nv) rv[i] = rr;
+    lds_barrier();
+    // stop when every equation is satisfied to its own scale (componentwise backward error,
+    // Oettli-Prager): |r - S x|_i <= 64 eps (|S| |x| + |r|)_i -- the level of the residual's own
+    // rounding; a normwise test lets the small (rotation) components of a badly scaled system drift
+    constexpr double kTol = 64.0 * 1.1102230246251565e-16;
+    double xi = warm_dot(Ir, rv + g * Qp);   // x_0 = S_t^-1 r
+    bool conv = false;
+    int it = 0;
+    for (;;) {
+        if (g == 0 && i < nv) x[i] = row ? xi : 0.0;
+        lds_barrier();
+        double sa;
+        const double res = rr - warm_dot_abs(Sr, x + g * Qp, sa);
+        const double q = fabs(res) - kTol * (sa + fabs(rr));   // <= 0: row i converged (NaN: not)
+        const double qm = wave_max(row ? (q == q ? q : 1.0) : -1.0);
+        if (g == 0 && i < nv) rv[i] = row ? res : 0.0;
+        if (lane == 0) red[wave] = qm;
+        lds_barrier();
+        {
+            double rd[nw];
+#pragma unroll
+            for (int k = 0; k < nw; ++k) rd[k] = red[k];
+            double qn = rd[0];
+#pragma unroll
+            for (int k = 1; k < nw; ++k) qn = fmax(qn, rd[k]);
+            conv = qn <= 0.0;
+        }
+        if (conv || it == kWarmMaxIters) break;
+        xi += warm_dot(Ir, rv + g * Qp);
+        ++it;
+    }
+    if (tid == 0) {
+        stats[0] += 1;
+        stats[1] += it;
+        if (!conv) stats[2] += 1;
+    }
+    return conv;
+}
+// The warm buffers are uncached device memory: plain loads and stores go to HBM whatever their
+// cache bits (so many loads stay in flight under the compiler's own waits); the epochs are read
+// and written with system-scope atomics so the spin loops re-load them.  The data loads follow
+// the epoch check through a workgroup barrier.
+__device__ __forceinline__ double2 ld_sys_x2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+__device__ __forceinline__ void st_sys_x2(double* p, double a, double b) {
+    f64x2_t v;
+    v.x = a;
+    v.y = b;
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ unsigned ld_sys_u32(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys_u32(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// no system will follow from this step (the loop stopped, a failed step): the helper may exit
+__device__ __forceinline__ void warm_stop(const WarmCtx& w) {
+    if (w.sync && threadIdx.x == 0) st_sys_u32(w.sync + 2, 1u);
+}
+
+// k_solve's m > 30 elimination with the warm path, in three pieces around solve_global's stop test
+// (so that its memory round trips overlap the state's):
+//   warm_issue  (every thread, before the stop test): this step's packed [S | r] into registers;
+//   warm_check  (thread 64, meanwhile): the epochs {published, inverted, stop, PD} in one 16-B load,
+//               a wait for the helper only if it has not inverted the last published system;
+//   warm_finish (after the stop test): stage [S | r] in LDS and publish it as sprev for the helper,
+//               load S_t^-1 (uncached) into LDS, refine; the direct elimination (gj_blocked) when
+//               there is no inverse yet, the helper is late, or the refinement does not converge;
+//               then the new epoch.  Barriers that only order LDS are raw s_barriers, so the sprev
+//               stores drain behind the refinement instead of at each barrier.
+// x: LDS (the solution), followed by the work area (mcc_solve_shmem).
+constexpr int kWarmPer = 8;   // double2 of [S | r] per thread: one pass up to m = 90 (2 093 double2 at 512 threads)
+struct WarmStage {
+    double2 v[kWarmPer];
+};
+__device__ __forceinline__ bool warm_on(const WarmCtx* w, int m) { return w && w->sync && m <= kWarmN; }
+__device__ __forceinline__ void warm_issue(const double* packed, int m, WarmStage& ws) {
+    const int n2 = warm_lc2(m), tid = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kWarmPer; ++u) {
+        const int q = u * (int)blockDim.x + tid;
+        ws.v[u] = q < n2 ? reinterpret_cast<const double2*>(packed)[q] : make_double2(0.0, 0.0);
+    }
+}
+__device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigned* e_s) {
+    const uint4 sy = *reinterpret_cast<const uint4*>(w.sync);   // {published, inverted, stop, PD}
+    const unsigned e = sy.x;
+    unsigned h = sy.y, ok = sy.w;
+    int use = 0;
+    if (e == 0) {
+        w.stats[3] += 1;
+    } else {
+        if (h != e) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (h != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < kWarmWaitTicks) {
+                __builtin_amdgcn_s_sleep(2);
+                h = ld_sys_u32(w.sync + 1);
+            }
+            ok = ld_sys_u32(w.sync + 3);
+        }
+        use = h == e && ok;
+        if (h != e) w.stats[4] += 1;   // the helper is late: direct elimination
+        else if (!use) w.stats[3] += 1;
+    }
+    *use_s = use;
+    *e_s = e;
+}
+__device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, int m, int* err, const WarmStage& ws,
+                            int use, unsigned e, int* bad_lds) {
+    const int tid = threadIdx.x, M = 16 * ((m + 15) / 16), n2 = warm_lc2(m);
+    double* Pk = x + kWarmN;                         // staged packed [S | r] (x: kWarmN doubles)
+    double* Iv = Pk + 2 * n2;                        // staged S_t^-1
+    double* work = Iv + (size_t)M * (M + 2);
+#pragma unroll
+    for (int u = 0; u < kWarmPer; ++u) {
+        const int q = u * (int)blockDim.x + tid;
+        if (q < n2) {
+            reinterpret_cast<double2*>(Pk)[q] = ws.v[u];
+            st_sys_x2(w.sprev + 2 * q, ws.v[u].x, ws.v[u].y);
+        }
+    }
+    bool solved = false;
+    if (use) {
+        // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
+        // rows of S_{t+1} from the staged packed system; then S_t^-1 into LDS, rows padded to
+        // M + 2 (16 rows of a wave would otherwise share banks)
+        constexpr int kIvPer = 9;   // double2 per thread: M x M / 2 <= 4 608 at 512 threads
+        const int n2i = M * M / 2;
+        double2 iv[kIvPer];
+#pragma unroll
+        for (int u = 0; u < kIvPer; ++u) {
+            const int q = u * (int)blockDim.x + tid;
+            iv[u] = q < n2i ? reinterpret_cast<const double2*>(w.sinv)[q] : make_double2(0.0, 0.0);
+        }
+        lds_barrier();   // the staged packed system
+        double Sr[kWarmQ];
+        warm_gather_s(Pk, m, Sr);
+#pragma unroll
+        for (int u = 0; u < kIvPer; ++u) {
+            const int q = u * (int)blockDim.x + tid;
+            if (q < n2i) {
+                const int t = 2 * q, r = t / M, c = t % M;
+                *reinterpret_cast<double2*>(Iv + r * (M + 2) + c) = iv[u];
+            }
+        }
+        lds_barrier();
+        solved = warm_refine(Sr, Iv, Pk, x, work, m, w.stats);
+    }
+    if (!solved) gj_blocked(packed, x, x + M, x + M + M * (M + 1), m, err, nullptr, bad_lds);
+    // publish this step's system (its sprev stores drained) for the helper
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (tid == 0) st_sys_u32(w.sync, e + 1u);
+}
+
+// In-place blocked Gauss-Jordan inverse of the padded SPD system in LDS (A: M x M, stride ld = M + 1,
+// 16 x 16 blocks; the helper).  Per pivot block kb: P^-1 (wave 0, gjb_inverse16); the pivot block row
+// A[kb][j] <- P^-1 A[kb][j]; every other block A[i][j] -= A[i][kb] A[kb][j]; the pivot block column
+// A[i][kb] <- -A[i][kb] P^-1 and A[kb][kb] <- P^-1.  Off the critical path (the step's linearisation
+// runs meanwhile), so no look-ahead.  Returns false (every thread) if a pivot is not > 0.
+__device__ bool gj_inverse_blocked(double* A, double* PV, int M) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int nb = M / 16, ld = M + 1;
+    __shared__ int bad_s;
+    if (tid == 0) bad_s = 0;
+    for (int kb = 0; kb < nb; ++kb) {
+        if (wave == 0 && !gjb_inverse16(A + 16 * kb * ld + 16 * kb, ld, PV, lane) && lane == 0) bad_s = 1;
+        __syncthreads();
+        for (int it = wave; it < nb - 1; it += nw) {   // pivot block row
+            const int jb = it < kb ? it : it + 1;
+            double* C = A + 16 * kb * ld + 16 * jb;
+            blk_mfma(C, ld, PV, kBlkLd, C, ld, false, true);
+        }
+        __syncthreads();
+        for (int it = wave; it < (nb - 1) * (nb - 1); it += nw) {   // the other blocks
+            const int r = it / (nb - 1), c = it % (nb - 1);
+            const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
+            blk_mfma(A + 16 * ib * ld + 16 * jb, ld, A + 16 * ib * ld + 16 * kb, ld, A + 16 * kb * ld + 16 * jb, ld,
+                     true, false);
+        }
+        __syncthreads();
+        for (int it = wave; it < nb; it += nw) {   // the pivot block column, and the pivot block
+            double* C = A + 16 * it * ld + 16 * kb;
+            if (it != kb) {
+                blk_mfma(C, ld, C, ld, PV, kBlkLd, true, true);
+            } else {
+                const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) C[i * ld + 4 * g + c] = PV[i * kBlkLd + 4 * g + c];
+            }
+        }
+        __syncthreads();
+    }
+    return bad_s == 0;
+}
+
+// The resident helper (one workgroup on a side stream, launched with each batch of update steps):
+// for each system k_solve publishes (sync[0] past the last one inverted), copy sprev into LDS,
+// invert it (gj_inverse_blocked), store S^-1 (uncached), drain, publish sync[1].  It exits after
+// n_systems systems, when a k_solve reports that no more systems follow (sync[2]: the loop
+// stopped, a failed step, a peer timeout), or after kHelperIdleTicks without a new system: every
+// wave reaches the exit.
+__global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m, int n_systems) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ unsigned ep_s;
+    __shared__ int quit_s;
+    const int tid = threadIdx.x, M = 16 * ((m + 15) / 16), ld = M + 1;
+    double* A = sm;
+    double* PV = sm + M * ld;
+    unsigned seen = ld_sys_u32(w.sync + 1);
+    for (int k = 0; k < n_systems; ++k) {
+        if (tid == 0) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            unsigned e = ld_sys_u32(w.sync);
+            int quit = 0;
+            while (e == seen) {
+                if (ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - t0 > kHelperIdleTicks) {
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+                e = ld_sys_u32(w.sync);
+            }
+            ep_s = e;
+            quit_s = quit;
+        }
+        __syncthreads();
+        if (quit_s) return;
+        const unsigned e = ep_s;
+        // sprev -> the full symmetric matrix in LDS (padding: identity)
+        const int ntri = m * (m + 1) / 2, n2 = (ntri + 1) / 2;
+        for (int q = tid; q < n2; q += blockDim.x) {
+            const double2 v = ld_sys_x2(w.sprev + 2 * q);
+            for (int h = 0; h < 2; ++h) {
+                const int t = 2 * q + h;
+                if (t < ntri) {
+                    int i, j;
+                    packed_ij(t, m, i, j);
+                    const double x = h ? v.y : v.x;
+                    A[i * ld + j] = x;
+                    A[j * ld + i] = x;
+                }
+            }
+        }
+        for (int t = tid; t < M * M; t += blockDim.x) {
+            const int i = t / M, j = t % M;
+            if (i >= m || j >= m) A[i * ld + j] = i == j ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        const bool ok = gj_inverse_blocked(A, PV, M);
+        for (int q = tid; q < M * M / 2; q += blockDim.x) {
+            const int t = 2 * q, i = t / M, j = t % M;
+            *reinterpret_cast<double2*>(w.sinv + t) = make_double2(A[i * ld + j], A[i * ld + j + 1]);
+        }
+        if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
+        // sinv is ordinary (cached) memory: write this XCD's L2 back before the epoch says it is there
+        // (k_solve reads it in a later launch, whose start drops stale lines from its own caches)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) st_sys_u32(w.sync + 1, e);
+        seen = e;
+    }
+}
+
+__device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err, int* bad_lds = nullptr) {
     switch (m) {
-#define GJ(M) case M: gj_rows<M>(S, r, m, lane, err); break;
+#define GJ(M) case M: gj_rows<M>(S, r, m, lane, err, bad_lds); break;
         GJ(6) GJ(12) GJ(18) GJ(24) GJ(30)
 #undef GJ
         default: break;
@@ -2622,14 +3020,25 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 
 // LARGE: m > 30 (k_solve only: the register-tiled elimination needs the whole workgroup's registers)
 template <bool LARGE>
-__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2) {
+__device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
+                                             const WarmCtx* warm) {
     State* st = a.state;
     const int m = a.m, tid = threadIdx.x;
     __shared__ int stop, s_iter;
     __shared__ double s_alpha;
     __shared__ float s_x[128];
+    __shared__ int s_use, s_bad, s_bad_rows, s_err0;
+    __shared__ unsigned s_ep;
     SSTAMP(a.stamps, 0, 0);
+    const bool wrm = LARGE && warm_on(warm, m);
+    WarmStage ws;
+    if (wrm) warm_issue(S, m, ws);
+    if (wrm && tid == 64) warm_check(*warm, &s_use, &s_ep);
     if (tid == 0) {
+        // the error bits the step's photo work set (bit 0), read with the state so that the stop
+        // at the end needs no further round trip
+        s_err0 = __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_bad = 0;
         const int k = st->iter;
         double change = 1.0;
         if (k > 0) {
@@ -2653,15 +3062,20 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         // speculative: the elimination does not depend on the stop test (its result is unused
         // when the loop stops), so wave 1 runs it while wave 0 loads the state
         SSTAMP(a.stamps, 1, 64);
-        gj_dispatch(S, r, m, tid - 64, &st->error);
+        if (tid == 64) s_bad_rows = 0;   // (this wave's own write below follows in program order)
+        gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
         SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();
-    if (stop) return;
+    if (stop) {
+        if (warm) warm_stop(*warm);
+        return;
+    }
     SSTAMP(a.stamps, 4, 0);
     if (LARGE) {   // S is the packed system itself (global); r (LDS) is followed by the block work area
         const int M = 16 * ((m + 15) / 16);
-        gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error, nullptr);
+        if (wrm) warm_finish(S, *warm, r, m, &st->error, ws, s_use, s_ep, &s_bad);
+        else gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error, nullptr, &s_bad);
     }
     SSTAMP(a.stamps, 5, 0);
     if (tid < 64) {
@@ -2696,7 +3110,10 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     // the steps after it, as mcc_check documents; the kernels test `done` only at their entry, so
     // no launch in flight loses a workgroup's ticket
     __syncthreads();
-    if (tid == 0 && (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 3)) st->done = 1;
+    if (tid == 0 && ((s_err0 & 3) || s_bad || (!LARGE && s_bad_rows))) {
+        st->done = 1;
+        if (warm) warm_stop(*warm);
+    }
 }
 
 // ---------------------------------------------------------------- k_schur
@@ -2841,15 +3258,21 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
 }
 
 // ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)
-__global__ __launch_bounds__(1024) void k_solve(SolveArgs a) {
-    if (a.ctx.state->done) return;
+__global__ __launch_bounds__(kSolveThreads) void k_solve(SolveArgs a) {
+    if (a.ctx.state->done) {
+        warm_stop(a.warm);
+        return;
+    }
     const int m = a.ctx.m, tid = threadIdx.x, ntri = m * (m + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;
     double* r = sm + m * m;
-    if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed, !a.pushed)) return;
+    if (a.peer.nranks > 0 && !peer_exchange(a.peer, a.ctx.state, a.packed, !a.pushed)) {
+        warm_stop(a.warm);
+        return;
+    }
     if (m > 30) {   // the blocked elimination reads the packed system directly (LDS: x, A, pivot inverse)
-        solve_global<true>(a.ctx, a.packed, sm, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
+        solve_global<true>(a.ctx, a.packed, sm, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1], &a.warm);
         return;
     }
     for (int t = tid; t < ntri; t += blockDim.x) {
@@ -3174,7 +3597,8 @@ size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp) {
 size_t mcc_solve_shmem(int m) {
     const size_t M = 16 * (size_t)((m + 15) / 16);
     const size_t blocked = M + M * (M + 1) + 2 * 16 * kBlkLd;   // gj_blocked (m > 30, k_solve)
-    return std::max((size_t)(m * m + m), m > 30 ? blocked : 0) * sizeof(double);
+    const size_t warm = M <= kWarmN ? kWarmN + warm_shmem_doubles(m) : 0;   // warm_finish
+    return std::max((size_t)(m * m + m), m > 30 ? std::max(blocked, warm) : 0) * sizeof(double);
 }
 
 hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
@@ -3266,8 +3690,10 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, siz
     if (ss > 60 * 1024) {
         hipError_t e1 = hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
         hipError_t e2 = hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
+        hipError_t e3 = hipFuncSetAttribute((const void*)&k_sinv_helper, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
         if (e1 != hipSuccess) err = e1;
         if (e2 != hipSuccess) err = e2;
+        if (e3 != hipSuccess) err = e3;
     }
     return err;
 }
@@ -3283,6 +3709,12 @@ hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
     // m > 30: 8 waves, so the block eliminations of a pivot step (up to (nb - 1)^2 16 x 16 MFMA
     // products) are not what waits on the next pivot inverse
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(a.ctx.m > 30 ? kSolveThreads : 256), mcc_solve_shmem(a.ctx.m), s, a);
+    return hipGetLastError();
+}
+hipError_t mcc_launch_sinv_helper(const WarmCtx& w, int m, int n_systems, hipStream_t s) {
+    const size_t M = 16 * (size_t)((m + 15) / 16);
+    const size_t shm = (M * (M + 1) + 16 * kBlkLd) * sizeof(double);
+    hipLaunchKernelGGL(k_sinv_helper, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
     return hipGetLastError();
 }
 hipError_t mcc_launch_peer_push(const PeerCtx& pc, const State* st, const double* vals, hipStream_t s) {
