@@ -349,9 +349,12 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     sa.nblk = p->nblk;
     sa.block_items = p->block_items.p;
     sa.packed = p->packed.p;
-    // m > 30: the register-tiled elimination runs in its own kernel (k_solve)
-    const bool split = rccl || peer || p->m > 30;
+    // m > 30: the register-tiled elimination runs in its own kernel (k_solve); with RCCL the
+    // all-reduce sits between k_schur and k_solve; with the peer transport and m <= 30, k_schur's
+    // final arriver exchanges and solves (no k_peer_push / k_solve launches)
+    const bool split = rccl || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
+    sa.peer = peer_ctx(p, peer && !split);
     sa.solve = solve_ctx(p, do_update);
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
     HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));

@@ -209,6 +209,7 @@ struct SchurArgs {
     int m, rank, fuse_solve;
     SolveCtx solve;
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
+    PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
 };
 
 // The m > 30 solve with the previous step's inverse (the "warm" solve, solve_large in

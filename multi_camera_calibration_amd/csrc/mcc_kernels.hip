@@ -3238,6 +3238,13 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         a.packed[ntri + 2 * m + w] = v;
     }
     if (!a.fuse_solve) return;
+    if (a.peer.nranks > 0) {
+        // multi-GPU, m <= 30: the rank-ordered sum of every rank's system right here (one launch
+        // fewer than k_peer_push + k_solve), then this rank solves it like the fused step does
+        __syncthreads();   // the norms above
+        if (!peer_exchange(a.peer, st, a.packed)) return;
+        if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
+    }
     STAMPP(a.stamps, 8, 3);
     for (int t = tid; t < ntri + m; t += blockDim.x) {
         const double v = ld_sc1(a.packed + t);

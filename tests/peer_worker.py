@@ -25,6 +25,9 @@ CASES = {
     "config3_small": lambda: rig.make_config("config3", n_views=48),
     # a shard without any observation of one camera (config2, 40 views, camera 3 on rank 0 only)
     "config2_nocam": lambda: rig.make_config("config2", n_views=40),
+    # m = 18 on the split step (MCC_FUSED=0: k_group -> k_schur, as each rank of bench.py's config4
+    # weak-scaling run takes at 1 000 views per rank): k_schur's final arriver exchanges and solves
+    "config4_split": lambda: rig.make_config("config4", n_views=64),
     # BASELINE.json's multi-GPU rigs at full size (bench.py's strong-scaling lines)
     "config3_full": lambda: rig.make_config("config3"),
     "config5_full": lambda: rig.make_config("config5"),
@@ -46,6 +49,8 @@ def main():
     case, rank, world, rdv, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
     steps = int(sys.argv[6]) if len(sys.argv) > 6 else 100
     p, mine, q = shard(case, world, rank)
+    if case.endswith("_split"):
+        os.environ["MCC_FUSED"] = "0"
     ba = api.BundleAdjuster(q, device=0)
     handles = api.file_allgather(os.path.join(rdv, "handles"), rank, world, ba.peer_handle())
     ba.peer_init(handles, world, rank)

@@ -32,7 +32,9 @@ for cfg in $STEPS; do
     f=$(find "$OUT/${cfg}_stats" -name "*kernel_stats.csv" | head -n 1)
     [ -n "$f" ] && cp "$f" "$OUT/${cfg}_kernel_stats.csv"
     echo "$cfg stats done"; cut -c1-120 "$OUT/${cfg}_kernel_stats.csv" | grep k_
-    ( cd /tmp && export TMPDIR=/tmp &&
+    # the PMC passes serialise the dispatches, so k_solve's warm-solve helper (a second, resident
+    # kernel) could only time out: they run with the direct solve (MCC_WARM=0)
+    ( cd /tmp && export TMPDIR=/tmp && export MCC_WARM=0 &&
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/${cfg}_fetch" -o run --output-format csv \
           -- python3 $B --steps $PS --warmup 4 --ramp-seconds 0.05 > "$OUT/${cfg}_fetch.log" 2>&1 &&
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/${cfg}_write" -o run --output-format csv \
