@@ -3228,12 +3228,24 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     double* r = sm + m * m;  // m
     __shared__ double norms[2];
     if (tid < 2) {
+        // every load in one memory round trip (the iteration count, the camera norm and the norm
+        // chunks' partials are independent), then the sums in chunk order as before
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
+        const int iter = st->iter;
+        const double cn = w ? st->cam_normX2 : st->cam_normG2;
+        constexpr int B = 32;
         double v = 0.0;
-        if (st->iter > 0) {
-            for (int k = a.n_items; k < (int)gridDim.x; ++k) v += ld_sc1(a.item_out + 48 * (size_t)k + w);
-            if (a.rank == 0) v += w ? st->cam_normX2 : st->cam_normG2;
+        for (int k0 = a.n_items; k0 < (int)gridDim.x; k0 += B) {
+            double pv[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                pv[u] = k0 + u < (int)gridDim.x ? ld_sc1(a.item_out + 48 * (size_t)(k0 + u) + w) : 0.0;
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (k0 + u < (int)gridDim.x) v += pv[u];
         }
+        if (a.rank == 0) v += cn;
+        if (iter <= 0) v = 0.0;
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
     }
