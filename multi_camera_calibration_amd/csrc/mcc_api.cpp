@@ -62,24 +62,32 @@ struct DevBuf {
 // Idle non-blocking streams per device, kept for the next problem: hipStreamDestroy costs ~2 ms
 // (most of an mcc_destroy) and creating one more than that.  A stream is returned only after it
 // has drained and its graphs and events are gone.
+// high: the warm solve's helper stream, at the highest stream priority, so that it never shares a
+// hardware queue with a step stream (streams are multiplexed onto a few queues per priority; a
+// resident helper kernel in a step stream's queue would hold that queue's later kernels back)
 struct StreamPool {
     std::mutex mu;
-    std::vector<std::pair<int, hipStream_t>> idle;   // (device, stream)
-    hipError_t take(int device, hipStream_t* s) {
+    std::vector<std::pair<int, hipStream_t>> idle;   // (device * 2 + high, stream)
+    hipError_t take(int device, hipStream_t* s, bool high = false) {
+        const int key = device * 2 + (high ? 1 : 0);
         {
             std::lock_guard<std::mutex> lk(mu);
             for (size_t i = 0; i < idle.size(); ++i)
-                if (idle[i].first == device) {
+                if (idle[i].first == key) {
                     *s = idle[i].second;
                     idle.erase(idle.begin() + (long)i);
                     return hipSuccess;
                 }
         }
-        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+        if (!high) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+        int least = 0, greatest = 0;
+        hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e != hipSuccess) return e;
+        return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
     }
-    void give(int device, hipStream_t s) {
+    void give(int device, hipStream_t s, bool high = false) {
         std::lock_guard<std::mutex> lk(mu);
-        idle.emplace_back(device, s);
+        idle.emplace_back(device * 2 + (high ? 1 : 0), s);
     }
 };
 StreamPool& stream_pool() {
@@ -183,6 +191,7 @@ struct mcc_problem {
     double* sprev = nullptr;         // uncached: packed [S | r]
     unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
+    int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
@@ -240,7 +249,8 @@ mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
 }
 
 mcc::WarmCtx warm_ctx(mcc_problem* p) {
-    return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->sprev, p->wsync, p->warm_stats.p};
+    return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->sprev, p->wsync, p->warm_stats.p,
+                        p->warm_poison};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
@@ -869,6 +879,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->use_group ? p->group_shmem : 0));
     p->warm = !p->fused && p->m > 30;
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
+    if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
     p->warm = p->warm && p->m <= 96;   // the staged system and inverse fit k_solve's LDS up to M = 96
     if (p->warm) {
         const size_t M = 16 * (size_t)((p->m + 15) / 16);
@@ -878,7 +889,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         HIPC(hipMemset(p->wsync, 0, 4 * sizeof(unsigned)));
         HIPC(p->warm_stats.alloc(5));
         HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
-        HIPC(stream_pool().take(d->device, &p->side));
+        HIPC(stream_pool().take(d->device, &p->side, true));
     }
 #undef HIPC
     (void)rc;
@@ -922,7 +933,7 @@ void mcc_destroy(mcc_problem* p) {
     if (p->h_state) (void)hipHostFree(p->h_state);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused
     else if (p->stream) (void)hipStreamDestroy(p->stream);
-    if (side_drained) stream_pool().give(p->device, p->side);
+    if (side_drained) stream_pool().give(p->device, p->side, true);
     else if (p->side) (void)hipStreamDestroy(p->side);
     delete p;
 }

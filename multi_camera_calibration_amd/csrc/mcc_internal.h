@@ -225,8 +225,10 @@ struct WarmCtx {
     double* sprev;           // [packed [S | r] rounded up to even] the last solved system, for the helper
     unsigned* sync;          // [3] epochs: systems published by k_solve, systems inverted by the helper; stop
     long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), helper late
+    int poison;              // test (MCC_WARM_POISON=1): the helper publishes a NaN inverse, so every
+                             // warm solve must fall back to the direct elimination
 };
-constexpr int kWarmMaxIters = 8;
+constexpr int kWarmMaxIters = 4;
 
 struct SolveArgs {
     SolveCtx ctx;

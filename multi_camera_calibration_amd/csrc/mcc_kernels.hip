@@ -2636,7 +2636,7 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
 constexpr int kWarmQ = 24;                 // M <= 96 (m <= 96): the staged S and S^-1 fit in LDS
 constexpr int kWarmN = 4 * kWarmQ;
 constexpr long long kWarmWaitTicks = 50000;        // k_solve waits <= 0.5 ms for the helper (100 MHz ticks)
-constexpr long long kHelperIdleTicks = 2000000;    // the helper exits after 20 ms without a new system
+constexpr long long kHelperIdleTicks = 500000;     // the helper exits after 5 ms without a new system
 __device__ __forceinline__ double wave_max(double v) {
     {
         double a = v, b = v;
@@ -2746,18 +2746,22 @@ __device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const 
     lds_barrier();
     // stop when every equation is satisfied to its own scale (componentwise backward error,
     // Oettli-Prager): |r - S x|_i <= 64 eps (|S| |x| + |r|)_i -- the level of the residual's own
-    // rounding; a normwise test lets the small (rotation) components of a badly scaled system drift
+    // rounding; a normwise test lets the small (rotation) components of a badly scaled system drift.
+    // (A fallback wastes the corrections it ran: it stops at kWarmMaxIters or at the first
+    // correction that does not cut the error fourfold.)
     constexpr double kTol = 64.0 * 1.1102230246251565e-16;
     double xi = warm_dot(Ir, rv + g * Qp);   // x_0 = S_t^-1 r
     bool conv = false;
     int it = 0;
+    double qprev = 0.0;
     for (;;) {
         if (g == 0 && i < nv) x[i] = row ? xi : 0.0;
         lds_barrier();
         double sa;
         const double res = rr - warm_dot_abs(Sr, x + g * Qp, sa);
-        const double q = fabs(res) - kTol * (sa + fabs(rr));   // <= 0: row i converged (NaN: not)
-        const double qm = wave_max(row ? (q == q ? q : 1.0) : -1.0);
+        // row i's componentwise backward error |r - S x|_i / (|S| |x| + |r|)_i (NaN: 1)
+        const double q = fabs(res) / fmax(sa + fabs(rr), 1e-300);
+        const double qm = wave_max(row ? (q == q ? q : 1.0) : 0.0);
         if (g == 0 && i < nv) rv[i] = row ? res : 0.0;
         if (lane == 0) red[wave] = qm;
         lds_barrier();
@@ -2768,9 +2772,13 @@ __device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const 
             double qn = rd[0];
 #pragma unroll
             for (int k = 1; k < nw; ++k) qn = fmax(qn, rd[k]);
-            conv = qn <= 0.0;
+            conv = qn <= kTol;
+            // give up early when a correction does not shrink the error fourfold (the systems moved
+            // too far for the stale inverse: the first Gauss-Newton steps from a rough start)
+            if (!conv && it > 0 && !(qn <= 0.25 * qprev)) it = kWarmMaxIters;
+            qprev = qn;
         }
-        if (conv || it == kWarmMaxIters) break;
+        if (conv || it >= kWarmMaxIters) break;
         xi += warm_dot(Ir, rv + g * Qp);
         ++it;
     }
@@ -2996,7 +3004,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         const bool ok = gj_inverse_blocked(A, PV, M);
         for (int q = tid; q < M * M / 2; q += blockDim.x) {
             const int t = 2 * q, i = t / M, j = t % M;
-            *reinterpret_cast<double2*>(w.sinv + t) = make_double2(A[i * ld + j], A[i * ld + j + 1]);
+            *reinterpret_cast<double2*>(w.sinv + t) =
+                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(A[i * ld + j], A[i * ld + j + 1]);
         }
         if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
         // sinv is ordinary (cached) memory: write this XCD's L2 back before the epoch says it is there

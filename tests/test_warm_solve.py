@@ -1,0 +1,110 @@
+"""The warm solve of the m > 30 reduced camera system: k_solve refines with
+the previous step's inverse, which the resident helper kernel computes while the next step
+linearises, and falls back to the direct elimination (the blocked Gauss-Jordan the oracle's
+Schur / Cholesky restatement is pinned against) when the refinement does not converge.  The solve
+it replaces is the reference's sparse CG on the whole normal equations
+(/root/reference/src/multicalib.cpp:565-592) inside optimizeExtrinsics (:462-514).
+
+  * warm on vs off (MCC_WARM=0): the same iteration count and final float32 parameters within 1 ulp,
+    both against the oracle's optimize at the single-GPU bars; the solve statistics show the warm
+    path ran (every update step after the first refines; no late helper);
+  * a NaN inverse (MCC_WARM_POISON=1) makes every warm solve fall back, and the fallback is the
+    direct elimination: bitwise the MCC_WARM=0 result;
+  * m = 126 (beyond the staged warm path's M <= 96) runs the direct elimination only.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from multi_camera_calibration_amd import api, rig
+from oracle import oracle_py as O
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ulp import f32_ulp_diff  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "config3_small": lambda: rig.make_config("config3", n_views=48),                # m = 90
+    "m48": lambda: rig.make_config("config3", n_cams=9, n_views=40),                 # m = 48
+    "m126": lambda: rig.make_config("config3", n_cams=22, n_views=120),              # m = 126: direct only
+}
+
+
+def run(p, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ba = api.BundleAdjuster(p)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        x, m, it, ch = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+        stats = ba.solve_stats()
+    finally:
+        ba.close()
+    return x, m, it, stats
+
+
+@pytest.mark.parametrize("name", ["config3_small", "m48"])
+def test_warm_matches_direct_and_oracle(name):
+    p = CASES[name]()
+    x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    xw, mw, itw, sw = run(p, {"MCC_WARM": "1"})
+    xd, md, itd, sd = run(p, {"MCC_WARM": "0"})
+    assert itw == itd == it_ref, (itw, itd, it_ref)
+    for x, m in ((xw, mw), (xd, md)):
+        assert abs(m - m_ref) <= 1e-6
+        assert f32_ulp_diff(x, x_ref).max() <= 1
+    assert f32_ulp_diff(xw, xd).max() <= 1
+    # every update step but the run's first tried the helper's inverse, none waited in vain; from a
+    # rough start the systems move too far between the first steps for the previous inverse (those
+    # fall back after a correction or two), so only the bench's steady state is required to refine
+    # (test_warm_steady_state)
+    assert sw["direct"] == 1 and sw["late"] == 0, sw
+    assert sw["warm"] + sw["direct"] >= itw, sw
+    assert sw["corrections"] <= 4 * sw["warm"], sw
+    assert sd == dict(warm=0, corrections=0, fallbacks=0, direct=0, late=0)
+
+
+def test_warm_fallback_is_the_direct_elimination():
+    p = CASES["config3_small"]()
+    xp, mp, itp, sp = run(p, {"MCC_WARM": "1", "MCC_WARM_POISON": "1"})
+    xd, md, itd, _ = run(p, {"MCC_WARM": "0"})
+    assert sp["warm"] > 0 and sp["fallbacks"] == sp["warm"], sp
+    assert itp == itd and mp == md
+    assert np.array_equal(xp, xd)
+
+
+def test_m126_direct_only():
+    p = CASES["m126"]()
+    x, m, it, s = run(p, {})
+    assert s == dict(warm=0, corrections=0, fallbacks=0, direct=0, late=0)
+
+
+def test_warm_steady_state():
+    """Free-running steps near convergence (the bench's loop): every solve after the first refines
+    with at most two corrections and none falls back."""
+    p = CASES["config3_small"]()
+    ba = api.BundleAdjuster(p)
+    try:
+        ba.set_params(p.x0)
+        ba.step(40)
+        ba.synchronize()
+        s0 = ba.solve_stats()
+        ba.step(64)
+        ba.synchronize()
+        ba.check()
+        s1 = ba.solve_stats()
+    finally:
+        ba.close()
+    warm = s1["warm"] - s0["warm"]
+    assert warm == 64, (s0, s1)
+    assert s1["fallbacks"] == s0["fallbacks"] and s1["late"] == 0, (s0, s1)
+    assert s1["corrections"] - s0["corrections"] <= 2 * warm, (s0, s1)
