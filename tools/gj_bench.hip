@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <random>
 #include <vector>
 
@@ -77,6 +78,8 @@ int main(int argc, char** argv) {
     std::sort(t.begin() + 1, t.end());
     double err = 0, xm = 0;
     for (int i = 0; i < m; ++i) { err = std::max(err, std::fabs(xg[i] - x[i])); xm = std::max(xm, std::fabs(x[i])); }
-    std::printf("m=%d gj median ticks %lld (min %lld, first %lld) rel err %.3e err flags %d\n", m, t[REPS / 2], t[1], t[0], err / xm, e);
+    unsigned long long h = 1469598103934665603ull;   // FNV-1a over the solution's bits (bitwise A/B)
+    for (int i = 0; i < m; ++i) { unsigned long long b; std::memcpy(&b, &xg[i], 8); h = (h ^ b) * 1099511628211ull; }
+    std::printf("m=%d gj median ticks %lld (min %lld, first %lld) rel err %.3e err flags %d bits %016llx\n", m, t[REPS / 2], t[1], t[0], err / xm, e, h);
     return 0;
 }
