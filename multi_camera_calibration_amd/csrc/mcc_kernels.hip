@@ -34,13 +34,19 @@
 namespace mcc {
 
 // ---------------------------------------------------------------- diagnostic stamps
-// Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
+// Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries
+// (-DMCC_DIAG_RT: the chip-wide 100 MHz s_memrealtime instead, for timelines across XCDs).
+#ifdef MCC_DIAG_RT
+#define MCC_DIAG_CLOCK() __builtin_amdgcn_s_memrealtime()
+#else
+#define MCC_DIAG_CLOCK() __builtin_amdgcn_s_memtime()
+#endif
 #ifdef MCC_DIAG
 #define STAMPP(ptr, stride, k)                                                                     \
     do {                                                                                           \
         if (threadIdx.x == 0 && (ptr)) {                                                           \
             __builtin_amdgcn_sched_barrier(0);                                                     \
-            (ptr)[(stride) * (size_t)blockIdx.x + (k)] = (long long)__builtin_amdgcn_s_memtime();  \
+            (ptr)[(stride) * (size_t)blockIdx.x + (k)] = (long long)MCC_DIAG_CLOCK();              \
             __builtin_amdgcn_sched_barrier(0);                                                     \
         }                                                                                          \
     } while (0)
@@ -54,7 +60,7 @@ namespace mcc {
     do {                                                                                           \
         if (threadIdx.x == (who) && (ptr)) {                                                       \
             __builtin_amdgcn_sched_barrier(0);                                                     \
-            (ptr)[k] = (long long)__builtin_amdgcn_s_memtime();                                    \
+            (ptr)[k] = (long long)MCC_DIAG_CLOCK();                                                \
             __builtin_amdgcn_sched_barrier(0);                                                     \
         }                                                                                          \
     } while (0)

@@ -4,6 +4,9 @@ workgroup ends, when k_schur's item workgroups start and finish, and the final w
 (ticks from the first k_group start, s_memtime).  Never quote this build's run time.
 
     MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so python tools/diag_schur.py [config] [views]
+
+With a -DMCC_DIAG_RT build (the chip-wide 100 MHz s_memrealtime; s_memtime is per XCD, so its
+cross-workgroup differences are meaningless) set MCC_DIAG_RT=1: times are then printed in us.
 """
 import os
 import sys
@@ -21,6 +24,14 @@ ba.set_params(p.x0)
 ba.step(20)
 ba.synchronize()
 ba.stamps()
+RT = os.environ.get("MCC_DIAG_RT") == "1"
+SC = 0.01 if RT else 1.0   # 100 MHz ticks -> us
+
+
+def q(v):
+    return f"{v * SC:.2f}" if RT else f"{v:.0f}"
+
+
 for rep in range(3):
     ba.step(1)
     ba.synchronize()
@@ -32,12 +43,15 @@ for rep in range(3):
     g0 = ph[:, 0][ph[:, 0] > 0]
     t0 = g0.min()
     gend = ph[:, 10][ph[:, 10] > 0]
-    print(f"rep {rep}: k_group {len(g0)} groups: start spread {g0.max() - t0}, end median {np.median(gend) - t0:.0f}, last {gend.max() - t0}")
+    print(f"rep {rep}: k_group {len(g0)} groups: start spread {q(g0.max() - t0)}, end median {q(np.median(gend) - t0)}, last {q(gend.max() - t0)}"
+          + (" (us)" if RT else " (ticks)"))
     fin = sch[sch[:, 7] > 0]
     items = sch[sch[:, 7] == 0]
     if len(items):
-        print(f"  k_schur items: {len(items)}, start min {items[:, 0].min() - t0}, items summed max {items[:, 1].max() - t0}, level-1 max {items[:, 2].max() - t0}")
+        lv1 = items[:, 2][items[:, 2] > 0]
+        print(f"  k_schur items: {len(items)}, start min {q(items[:, 0].min() - t0)} max {q(items[:, 0].max() - t0)}, "
+              f"items summed max {q(items[:, 1].max() - t0)}, level-1 max {q(lv1.max() - t0) if len(lv1) else '-'}")
     for f in fin:
         names = ["solve entry", "GJ start (w1)", "GJ end (w1)", "final: before packed loads", "stop-test barrier", "-", "camera update", "end"]
-        print("  final WG: " + ", ".join(f"{n} {v - t0}" for n, v in zip(names, f) if v))
+        print("  final WG: " + ", ".join(f"{n} {q(v - t0)}" for n, v in zip(names, f) if v))
 ba.close()
