@@ -43,6 +43,7 @@ extern "C" {
 #define MCC_ENOTPD (-3)     /* a normal-equation block is not positive definite  */
 #define MCC_ECOMM (-4)      /* RCCL error                                        */
 #define MCC_ENOMEM (-5)
+#define MCC_ETIMEOUT (-6)   /* a device-side wait timed out (the m > 30 warm-solve helper)     */
 
 /* Camera model / class semantics the linearisation follows. */
 #define MCC_MODEL_PINHOLE 0     /* MyMultiCameraCalibration, cv::projectPoints (k1..k6,p1,p2,s1..s4) */
@@ -160,9 +161,11 @@ int mcc_peer_enable(mcc_problem *p, int on);
 /* the m > 30 split step's warm solves since mcc_create (k_solve refines with the previous step's
  * inverse, which a resident helper kernel computes while the step linearises): out[5] = {solves by
  * refinement, refinement corrections in them, refinements that did not converge (the direct
- * elimination ran instead), direct solves for want of an inverse (a run's first step), direct
- * solves because the helper was late}; all zero when the problem takes the direct elimination only
- * (m <= 30, m > 96, MCC_WARM=0) */
+ * elimination ran instead), direct solves for want of an inverse (an optimisation's first step, or
+ * the previous system was not positive definite), solves that had to wait for the helper}; all zero
+ * when the problem takes the direct elimination only (m <= 30, m > 96, MCC_WARM=0).  Which solve a
+ * step takes depends on the systems only, never on timing: a step waits for the helper as long as
+ * needed, up to MCC_WARM_TIMEOUT_MS (default 10000), after which it fails with MCC_ETIMEOUT. */
 int mcc_solve_stats(mcc_problem *p, long long *out);
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);

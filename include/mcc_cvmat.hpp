@@ -10,12 +10,13 @@
  * col are views into the parent), element access (at, ptr), convertTo, t(), matrix products,
  * element-wise + / -, scalar scaling and cv::norm.  Type codes follow OpenCV (CV_32F = 5,
  * CV_64F = 6, CV_MAKETYPE(depth, cn) = depth + ((cn - 1) << 3)).  No OpenCV code is used or
- * needed; when a translation unit includes the real OpenCV first, this shim is skipped
- * (MCC_HAVE_OPENCV) -- the two cannot coexist.
+ * needed.  It replaces OpenCV: include/opencv2/ccalib/multicalib.hpp refuses to compile after the real
+ * OpenCV headers (#error), since the seam reads matrices through this shim's accessors.
  */
 #ifndef MCC_CVMAT_HPP
 #define MCC_CVMAT_HPP
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -162,6 +163,11 @@ public:
         if (dst.rows != rows || dst.cols != cols || dst.type_ != type_ || !dst.buf_) dst.create(rows, cols, type_);
         for (int r = 0; r < rows; ++r) std::memcpy(dst.ptr<unsigned char>(r), ptr<unsigned char>(r), (size_t)cols * elemSize());
     }
+    // into a temporary view, as OpenCV's OutputArray allows: m.copyTo(J.rowRange(a, b).colRange(c, d))
+    void copyTo(Mat&& dst) const {
+        Mat d = dst;
+        copyTo(d);
+    }
     void convertTo(Mat& dst, int rtype, double alpha = 1.0) const {
         const int cn = channels();
         Mat out(rows, cols, CV_MAKETYPE(rtype & 7, cn));
@@ -200,6 +206,21 @@ public:
         b.one_channel();
         if (a.cols != b.rows || a.depth() != b.depth()) throw std::invalid_argument("cv::Mat: product size / type");
         Mat m(a.rows, b.cols, a.type_);
+        if (a.depth() == CV_64F) {   // row-major i-k-j: each output row accumulates over k in order
+            std::vector<double> acc(b.cols);
+            for (int i = 0; i < a.rows; ++i) {
+                std::fill(acc.begin(), acc.end(), 0.0);
+                const double* ai = a.ptr<double>(i);
+                for (int k = 0; k < a.cols; ++k) {
+                    const double aik = ai[k];
+                    if (aik == 0.0) continue;   // exact: the dense J of a BA problem is mostly zeros
+                    const double* bk = b.ptr<double>(k);
+                    for (int j = 0; j < b.cols; ++j) acc[j] += aik * bk[j];
+                }
+                std::copy(acc.begin(), acc.end(), m.ptr<double>(i));
+            }
+            return m;
+        }
         for (int i = 0; i < a.rows; ++i)
             for (int j = 0; j < b.cols; ++j) {
                 double s = 0.0;

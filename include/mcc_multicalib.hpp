@@ -148,6 +148,41 @@ inline bool strict_reference_env() {
     std::abort();
 }
 
+// ---- one edge's linearisation on the host (libmcc_host.so, host/edge_jacobian.cpp): the reference's
+// per-edge computePhotoCameraJacobian for callers that assemble their own normal equations the way
+// the reference's computeJacobianExtrinsic does (the cv::Mat seam's subclasses).  The library's own
+// classes linearise whole steps on the GPU (mcc_linearize_solve) and never call it.
+enum { EDGE_BASE = 0, EDGE_MYMULTI = 1, EDGE_DOUBLESIDE = 2 };   // src/multicalib.cpp:717, mymulticalib.cpp:468, doubleSide.cpp:288
+struct EdgeLinearization {
+    std::vector<double> jacPhoto;    // [2N x 6] row-major, rows u0, v0, u1, ...: d/d(rvec, tvec) of the photo
+    std::vector<double> jacGlobal;   // [2N x 6]: of the camera (EDGE_BASE, EDGE_MYMULTI) or ds (EDGE_DOUBLESIDE)
+    std::vector<double> E;           // [2N]: fl32(obs - proj) widened to double
+    std::vector<float> proj;         // [2N]: the float32 projected corners
+    double rvecTran[3], tvecTran[3];     // the composed pose (FP64)
+    float rvecTranF[3], tvecTranF[3];    // the pose projected (rounded to float32, :546-553)
+};
+// compose_motion (src/multicalib.cpp:1008-1056): om3, T3 and the partials d[8] in the reference's
+// order dom3dom1, dom3dT1, dom3dom2, dom3dT2, dT3dom1, dT3dT1, dT3dom2, dT3dT2 (row-major 3 x 3)
+void composeMotion(const double om1[3], const double T1[3], const double om2[3], const double T2[3], double om3[3],
+                   double T3[3], double d[8][9]);
+// one edge: photo (rP, tP), camera (rC, tC), the double-side transform (rDs, tDs; BACK views of
+// EDGE_MYMULTI / EDGE_DOUBLESIDE), n corners obj[3n] / img[2n], K row-major, D[nd], xi (omni)
+void edgeJacobian(int edgeClass, bool omni, int patternSide, const double rP[3], const double tP[3],
+                  const double rC[3], const double tC[3], const double* rDs, const double* tDs, int n,
+                  const float* obj, const float* img, const float K[9], const float* D, int nd, float xi,
+                  EdgeLinearization& out);
+
+}  // namespace multicalib
+}  // namespace mcc
+// the same for C callers (jac_photo / jac_global [12 n], E [2 n], pose_f32 [6]: the projected pose;
+// each may be NULL); 0 or MCC_EINVAL
+extern "C" int mcc_host_edge_jacobian(int edge_class, int omni, int pattern_side, const double* rP, const double* tP,
+                                      const double* rC, const double* tC, const double* rDs, const double* tDs, int n,
+                                      const float* obj, const float* img, const float* K, const float* D, int nd,
+                                      float xi, double* jac_photo, double* jac_global, double* E, float* pose_f32);
+namespace mcc {
+namespace multicalib {
+
 class MultiCameraCalibration {
 public:
     enum { PINHOLE, OMNIDIRECTIONAL };            // multicalib.hpp:76-79

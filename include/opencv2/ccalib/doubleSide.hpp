@@ -29,17 +29,41 @@ public:
     using detail::Seam<mcc::multicalib::DoubleSideCalibration, DoubleSideCalibration>::Seam;
 
 protected:
-    // computePhotoCameraJacobian (doubleSide.hpp:153-157, src/doubleSide.cpp:288-430); see multicalib.hpp
+    // computePhotoCameraJacobian (doubleSide.hpp:153-157, src/doubleSide.cpp:288-430): one edge's
+    // Jacobians w.r.t. the photo and the double-side transform (zero for FRONT views, :335-336),
+    // the residual; rvecTran / tvecTran are left as they are
     virtual void computePhotoCameraJacobian(int patternSide, const Mat& rvecPhoto, const Mat& tvecPhoto,
                                             const Mat& rvecCamera, const Mat& tvecCamera,
                                             const Mat& rvecDoubleside, const Mat& tvecDoubleside, Mat& rvecTran,
                                             Mat& tvecTran, const Mat& objectPoints, const Mat& imagePoints,
                                             const Mat& K, const Mat& distort, const Mat& xi, Mat& jacobianPhoto,
                                             Mat& jacobianDoubleside, Mat& E) {
-        (void)patternSide; (void)rvecPhoto; (void)tvecPhoto; (void)rvecCamera; (void)tvecCamera;
-        (void)rvecDoubleside; (void)tvecDoubleside; (void)rvecTran; (void)tvecTran; (void)objectPoints;
-        (void)imagePoints; (void)K; (void)distort; (void)xi; (void)jacobianPhoto; (void)jacobianDoubleside; (void)E;
-        no_per_edge_jacobian();
+        (void)rvecTran; (void)tvecTran;
+        detail::edge_jacobian_mats(mcc::multicalib::EDGE_DOUBLESIDE, false, patternSide, rvecPhoto, tvecPhoto,
+                                   rvecCamera, tvecCamera, &rvecDoubleside, &tvecDoubleside, objectPoints, imagePoints,
+                                   K, distort, xi, jacobianPhoto, jacobianDoubleside, E, nullptr, nullptr);
+    }
+    // camerasPose_rvec[c] / camerasPose_tvec[c] (doubleSide.hpp:124-125; cameraPose2vec,
+    // src/doubleSide.cpp:262-275): the fixed CV_32F camera pose as rvec, tvec (3 x 1 CV_32F)
+    Mat camerasPose_rvec(int camera) const {
+        float r[3];
+        mcc::multicalib::rodrigues_m2v(rotation_of(this->camerasPose.at(camera)).data(), r);
+        Mat m(3, 1, CV_32F);
+        for (int k = 0; k < 3; ++k) m.at<float>(k, 0) = r[k];
+        return m;
+    }
+    Mat camerasPose_tvec(int camera) const {
+        Mat m(3, 1, CV_32F);
+        for (int k = 0; k < 3; ++k) m.at<float>(k, 0) = this->camerasPose.at(camera)[4 * k + 3];
+        return m;
+    }
+
+private:
+    static std::array<float, 9> rotation_of(const mcc::multicalib::Pose& P) {
+        std::array<float, 9> R;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[3 * i + j] = P[4 * i + j];
+        return R;
     }
 };
 

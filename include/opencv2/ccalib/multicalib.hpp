@@ -28,14 +28,24 @@
  * and in strict-reference mode it is the reference's loop (src/multicalib.cpp:462-514) on the host,
  * calling this object's virtual computeJacobianExtrinsic (by default one GPU linearisation + solve),
  * computeProjectError, buildParas and paras2vertex exactly where the reference does.
- * computePhotoCameraJacobian is the reference's per-edge CPU Jacobian; this build linearises whole
- * steps on the GPU and never calls it, so its default throws std::logic_error: a subclass that
- * supplies one must also override computeJacobianExtrinsic to use it (as the reference's MyMulti
- * and DoubleSide do).  Build: -I<repo>/include/opencv2/ccalib -I<repo>/include, link
- * -lmcc_host -lmcc.
+ * computePhotoCameraJacobian is the reference's per-edge CPU Jacobian (base :717-824, MyMulti
+ * src/mymulticalib.cpp:468-614, DoubleSide src/doubleSide.cpp:288-430), restated on the host
+ * (mcc::multicalib::edgeJacobian, libmcc_host.so): the library's own loop linearises whole steps on
+ * the GPU and never calls it, but a subclass whose computeJacobianExtrinsic assembles the dense J
+ * edge by edge the way the reference's does gets the reference's per-edge blocks from it.  The
+ * per-view state such a body reads is offered as cv::Mat too (objectPointsMat, imagePointsMat,
+ * cameraMatrixMat, distortCoeffsMat, xiMat, transformMat; MyMulti's doubleSideTransform_rvec /
+ * _tvec, DoubleSide's camerasPose_rvec / _tvec as functions).  Build: -I<repo>/include/opencv2/ccalib
+ * -I<repo>/include, link -lmcc_host -lmcc.
  */
 #ifndef MCC_CV_MULTICALIB_HPP
 #define MCC_CV_MULTICALIB_HPP
+
+#if defined(OPENCV_CORE_HPP) || defined(OPENCV_CORE_MAT_HPP)
+// the seam reads cv::Mat through the in-repo shim's accessors (mcc_cvmat.hpp): it is this build's
+// stand-in for OpenCV, not an extension of it
+#error "include/opencv2/ccalib/*.hpp replace OpenCV's cv::multicalib headers; do not include OpenCV before them"
+#endif
 
 #include <cstdio>
 #include <iostream>
@@ -111,6 +121,59 @@ inline Mat mat33(const double* v) {
 }
 inline void vec3(const Mat& m, double v[3]) {
     for (int k = 0; k < 3; ++k) v[k] = m.rows == 1 ? m.get(0, k) : m.get(k, 0);
+}
+// every scalar of a matrix (any channel count) in row-major order, as float
+inline std::vector<float> flat_f32(const Mat& m) {
+    std::vector<float> v;
+    v.reserve(m.total() * m.channels());
+    for (int r = 0; r < m.rows; ++r)
+        for (int c = 0; c < m.cols * m.channels(); ++c)
+            v.push_back(m.depth() == CV_64F ? (float)m.ptr<double>(r)[c] : m.ptr<float>(r)[c]);
+    return v;
+}
+inline Mat rows_f32(const std::vector<float>& v, int width) {   // n x width CV_32F
+    Mat m((int)(v.size() / width), width, CV_32F);
+    for (size_t i = 0; i < v.size(); ++i) m.at<float>((int)(i / width), (int)(i % width)) = v[i];
+    return m;
+}
+// the reference's per-edge computePhotoCameraJacobian on cv::Mat arguments: jacobianPhoto /
+// jacobianGlobal (2N x 6 CV_64F), E (2N x 1 CV_64F, rows u0, v0, u1, ...); rvecTran / tvecTran
+// (3 x 1 CV_32F) when given (the base class's version assigns them, MyMulti's and DoubleSide's do not)
+inline void edge_jacobian_mats(int edgeClass, bool omni, int patternSide, const Mat& rP, const Mat& tP, const Mat& rC,
+                               const Mat& tC, const Mat* rDs, const Mat* tDs, const Mat& objectPoints,
+                               const Mat& imagePoints, const Mat& K, const Mat& distort, const Mat& xi,
+                               Mat& jacobianPhoto, Mat& jacobianGlobal, Mat& E, Mat* rvecTran, Mat* tvecTran) {
+    double rp[3], tp[3], rc[3], tc[3], rd[3] = {0, 0, 0}, td[3] = {0, 0, 0};
+    vec3(rP, rp); vec3(tP, tp); vec3(rC, rc); vec3(tC, tc);
+    const bool ds = rDs && tDs && !rDs->empty() && !tDs->empty();
+    if (ds) { vec3(*rDs, rd); vec3(*tDs, td); }
+    const std::vector<float> obj = flat_f32(objectPoints), img = flat_f32(imagePoints), k = flat_f32(K);
+    const std::vector<float> d = flat_f32(distort);
+    const int n = (int)(obj.size() / 3);
+    if (obj.size() != 3 * (size_t)n || img.size() != 2 * (size_t)n || k.size() != 9)
+        throw std::runtime_error("computePhotoCameraJacobian: objectPoints N x 3, imagePoints N x 2, K 3 x 3");
+    const float xif = omni && !xi.empty() ? flat_f32(xi)[0] : 0.f;
+    mcc::multicalib::EdgeLinearization L;
+    mcc::multicalib::edgeJacobian(edgeClass, omni, patternSide, rp, tp, rc, tc, ds ? rd : nullptr, ds ? td : nullptr, n,
+                                  obj.data(), img.data(), k.data(), d.data(), (int)d.size(), xif, L);
+    jacobianPhoto = Mat(2 * n, 6, CV_64F);
+    jacobianGlobal = Mat(2 * n, 6, CV_64F);
+    E = Mat(2 * n, 1, CV_64F);
+    for (int r = 0; r < 2 * n; ++r) {
+        for (int c = 0; c < 6; ++c) {
+            jacobianPhoto.at<double>(r, c) = L.jacPhoto[6 * (size_t)r + c];
+            jacobianGlobal.at<double>(r, c) = L.jacGlobal[6 * (size_t)r + c];
+        }
+        E.at<double>(r, 0) = L.E[r];
+    }
+    if (rvecTran && tvecTran) {
+        *rvecTran = Mat(3, 1, CV_32F);
+        *tvecTran = Mat(3, 1, CV_32F);
+        for (int q = 0; q < 3; ++q) {
+            rvecTran->at<float>(q, 0) = L.rvecTranF[q];
+            tvecTran->at<float>(q, 0) = L.tvecTranF[q];
+        }
+    }
 }
 
 // The reference's cv::Mat-typed seam over one of the host layer's classes (Impl), for the
@@ -324,12 +387,26 @@ protected:
         }
         return true;
     }
-    [[noreturn]] static void no_per_edge_jacobian() {
-        throw std::logic_error(
-            "computePhotoCameraJacobian: this build linearises whole Gauss-Newton steps on the GPU "
-            "(computeJacobianExtrinsic) and provides no per-edge CPU Jacobian; a subclass that "
-            "supplies one must also override computeJacobianExtrinsic to use it");
+    // the per-view state (multicalib.hpp:207-214) as the reference's cv::Mat types, for a subclass
+    // body written against them: corners N x 3 / N x 2 CV_32F, K 3 x 3, distortion 1 x nd, xi 1 x 1,
+    // an edge's transform 4 x 4 (all CV_32F, copies)
+    Mat objectPointsMat(int camera, int photoIndex) const {
+        return rows_f32(this->_objectPointsForEachCamera.at(camera).at(photoIndex), 3);
     }
+    Mat imagePointsMat(int camera, int photoIndex) const {
+        return rows_f32(this->_imagePointsForEachCamera.at(camera).at(photoIndex), 2);
+    }
+    Mat cameraMatrixMat(int camera) const {
+        const auto& k = this->_cameraMatrix.at(camera);
+        return rows_f32(std::vector<float>(k.begin(), k.end()), 3);
+    }
+    Mat distortCoeffsMat(int camera) const {
+        const auto& d = this->_distortCoeffs.at(camera);
+        return rows_f32(d, (int)std::max<size_t>(d.size(), 1));
+    }
+    Mat xiMat(int camera) const { return rows_f32(std::vector<float>(1, this->_xi.at(camera)), 1); }
+    template <class Edge>
+    Mat transformMat(const Edge& e) const { return rows_f32(std::vector<float>(e.transform.begin(), e.transform.end()), 4); }
 };
 
 }  // namespace detail
@@ -340,16 +417,17 @@ public:
     using detail::Seam<mcc::multicalib::MultiCameraCalibration, MultiCameraCalibration>::Seam;
 
 protected:
-    // computePhotoCameraJacobian (multicalib.hpp:178-180): the base class's per-edge Jacobian
+    // computePhotoCameraJacobian (multicalib.hpp:178-180, src/multicalib.cpp:717-824): one edge's
+    // Jacobians w.r.t. the photo and the camera, the residual, and the composed pose (CV_32F) in
+    // rvecTran / tvecTran; the camera model is _camType's (projectPoints / omnidir::projectPoints)
     virtual void computePhotoCameraJacobian(const Mat& rvecPhoto, const Mat& tvecPhoto, const Mat& rvecCamera,
                                             const Mat& tvecCamera, Mat& rvecTran, Mat& tvecTran,
                                             const Mat& objectPoints, const Mat& imagePoints, const Mat& K,
                                             const Mat& distort, const Mat& xi, Mat& jacobianPhoto,
                                             Mat& jacobianCamera, Mat& E) {
-        (void)rvecPhoto; (void)tvecPhoto; (void)rvecCamera; (void)tvecCamera; (void)rvecTran; (void)tvecTran;
-        (void)objectPoints; (void)imagePoints; (void)K; (void)distort; (void)xi; (void)jacobianPhoto;
-        (void)jacobianCamera; (void)E;
-        no_per_edge_jacobian();
+        detail::edge_jacobian_mats(mcc::multicalib::EDGE_BASE, this->_camType == OMNIDIRECTIONAL, FRONT_PATTERN,
+                                   rvecPhoto, tvecPhoto, rvecCamera, tvecCamera, nullptr, nullptr, objectPoints,
+                                   imagePoints, K, distort, xi, jacobianPhoto, jacobianCamera, E, &rvecTran, &tvecTran);
     }
 };
 

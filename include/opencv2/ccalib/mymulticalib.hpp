@@ -19,6 +19,7 @@
 #define MCC_CV_MYMULTICALIB_HPP
 
 #include "multicalib.hpp"
+#include "../../mcc_pnp.hpp"
 
 using namespace cv;
 
@@ -31,18 +32,36 @@ public:
     using detail::Seam<mcc::multicalib::MyMultiCameraCalibration, MyMultiCameraCalibration>::Seam;
 
 protected:
-    // computePhotoCameraJacobian (mymulticalib.hpp:166-170): one edge's Jacobians with the
-    // double-side transform of BACK views (src/mymulticalib.cpp:468-614); see multicalib.hpp
+    // computePhotoCameraJacobian (mymulticalib.hpp:166-170, src/mymulticalib.cpp:468-614): one edge's
+    // Jacobians w.r.t. the photo and the camera (BACK views through compose(ds, photofront), chained
+    // as :509-517 chain them), the residual; Rvectran / Tvectran are left as they are (the reference
+    // projects local copies)
     virtual void computePhotoCameraJacobian(int patternSide, const Mat& RvecPhoto, const Mat& TvecPhoto,
                                             const Mat& RvecCamera, const Mat& TvecCamera,
                                             const Mat& RvecDoubleside, const Mat& TvecDoubleside, Mat& Rvectran,
                                             Mat& Tvectran, const Mat& objectPoints, const Mat& imagePoints,
                                             const Mat& K, const Mat& distort, const Mat& xi, Mat& jacobianPhoto,
                                             Mat& jacobianDoubleside, Mat& E) {
-        (void)patternSide; (void)RvecPhoto; (void)TvecPhoto; (void)RvecCamera; (void)TvecCamera;
-        (void)RvecDoubleside; (void)TvecDoubleside; (void)Rvectran; (void)Tvectran; (void)objectPoints;
-        (void)imagePoints; (void)K; (void)distort; (void)xi; (void)jacobianPhoto; (void)jacobianDoubleside; (void)E;
-        no_per_edge_jacobian();
+        (void)Rvectran; (void)Tvectran;
+        detail::edge_jacobian_mats(mcc::multicalib::EDGE_MYMULTI, false, patternSide, RvecPhoto, TvecPhoto, RvecCamera,
+                                   TvecCamera, &RvecDoubleside, &TvecDoubleside, objectPoints, imagePoints, K, distort,
+                                   xi, jacobianPhoto, jacobianDoubleside, E, nullptr, nullptr);
+    }
+    // doubleSideTransform_rvec / _tvec (mymulticalib.hpp:123; doublesideTransform2vec,
+    // src/mymulticalib.cpp:105-117): the CV_64F transform as rvec, tvec (3 x 1 CV_64F)
+    Mat doubleSideTransform_rvec() const {
+        double R[9], r[3];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[3 * i + j] = this->doubleSideTransform[4 * i + j];
+        mcc::pnp::rodriguesInv(R, r);
+        Mat m(3, 1, CV_64F);
+        for (int k = 0; k < 3; ++k) m.at<double>(k, 0) = r[k];
+        return m;
+    }
+    Mat doubleSideTransform_tvec() const {
+        Mat m(3, 1, CV_64F);
+        for (int k = 0; k < 3; ++k) m.at<double>(k, 0) = this->doubleSideTransform[4 * k + 3];
+        return m;
     }
 };
 

@@ -339,11 +339,11 @@ class BundleAdjuster:
     def solve_stats(self):
         """The m > 30 warm solves (mcc_solve_stats): solves by refinement with the previous step's
         inverse, their refinement corrections, refinements that fell back to the direct elimination,
-        direct solves for want of an inverse, direct solves because the helper was late (all zero on
-        the direct-only paths)."""
+        direct solves for want of an inverse, solves that waited for the helper (the choice of solve
+        never depends on the wait; all zero on the direct-only paths)."""
         v = (ctypes.c_longlong * 5)()
         _check(lib().mcc_solve_stats(self.h, v), "mcc_solve_stats")
-        return dict(warm=v[0], corrections=v[1], fallbacks=v[2], direct=v[3], late=v[4])
+        return dict(warm=v[0], corrections=v[1], fallbacks=v[2], direct=v[3], waited=v[4])
 
     def path(self):
         """'fused' (one kernel per step) or 'split' (k_prep, k_edge, k_photo, k_schur, k_solve)."""

@@ -192,6 +192,11 @@ struct mcc_problem {
     unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
+    // k_solve's bound on the wait for the helper (MCC_WARM_TIMEOUT_MS, default 10 s; a step that hits
+    // it fails with MCC_ETIMEOUT), the helper's idle exit (the wait bound plus the peer timeout: a
+    // k_solve may sit in a peer exchange before it publishes), the test delay (MCC_WARM_DELAY_US)
+    long long warm_wait_ticks = 1000000000LL, warm_idle_ticks = 4000000000LL, warm_delay_ticks = 0;
+    int fault_photo = -1;            // MCC_FAULT_PHOTO (test): LinArgs::fault_photo
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
     DevBuf<int4> edge_info, items, gpairs;
@@ -250,7 +255,7 @@ mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
 
 mcc::WarmCtx warm_ctx(mcc_problem* p) {
     return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->sprev, p->wsync, p->warm_stats.p,
-                        p->warm_poison};
+                        p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
@@ -303,6 +308,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.dg = p->dg.p;
     la.photo_norm = p->photo_norm.p;
     la.stamps = p->stamps.p;
+    la.fault_photo = p->fault_photo;
     // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
     // split path: the packed system is summed by RCCL and solved by k_solve.  The peer transport
     // keeps one kernel per step: the final arriver exchanges with the peers and solves.
@@ -419,27 +425,38 @@ int build_graph(mcc_problem* p, int k) {
 }
 int launch_update_steps(mcc_problem* p, int n) {
     if (p->timing_window) p->win_steps += n;
+    const bool eager = p->timing || !p->use_graph;
+    // every graph of this batch exists before the batch's helper starts: instantiating a 64-step
+    // graph takes milliseconds, which the helper would otherwise spend polling for the first system
+    if (!eager)
+        for (int k = p->graph_sizes - 1, r = n; k >= 0; --k)
+            if (r >= (1 << k)) {
+                int rc = build_graph(p, k);
+                if (rc) return rc;
+                r -= (r >> k) << k;
+            }
     if (p->warm && n > 0) {
         // the batch's helper: after the previous one (side-stream order), with the stop flag cleared
         HIPCHK(hipMemsetAsync(p->wsync + 2, 0, sizeof(unsigned), p->side));
         HIPCHK(mcc_launch_sinv_helper(warm_ctx(p), p->m, n, p->side));
     }
-    if (p->timing || !p->use_graph) {
-        for (int i = 0; i < n; ++i) {
-            int rc = enqueue_step(p, 1, nullptr);
-            if (rc) return rc;
-        }
-        return MCC_OK;
+    int rc = MCC_OK;
+    if (eager) {
+        for (int i = 0; i < n && rc == MCC_OK; ++i) rc = enqueue_step(p, 1, nullptr);
+    } else {
+        for (int k = p->graph_sizes - 1; k >= 0 && rc == MCC_OK; --k)
+            while (n >= (1 << k) && rc == MCC_OK) {
+                hipError_t e = hipGraphLaunch(p->gexec[k], p->stream);
+                if (e != hipSuccess) rc = fail(MCC_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+                n -= 1 << k;
+            }
     }
-    for (int k = p->graph_sizes - 1; k >= 0; --k) {
-        while (n >= (1 << k)) {
-            int rc = build_graph(p, k);
-            if (rc) return rc;
-            HIPCHK(hipGraphLaunch(p->gexec[k], p->stream));
-            n -= 1 << k;
-        }
+    if (rc != MCC_OK && p->warm) {
+        // the steps that would have fed the helper were not enqueued: release it (uncached flag)
+        const unsigned one = 1;
+        (void)hipMemcpy(p->wsync + 2, &one, sizeof(one), hipMemcpyHostToDevice);
     }
-    return MCC_OK;
+    return rc;
 }
 
 int read_state(mcc_problem* p);
@@ -448,6 +465,13 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     p->stepping = false;
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
+    if (reset_iter && p->warm) {
+        // a new optimisation starts without a previous inverse (its first solve is the direct
+        // elimination), so its result does not depend on what the problem solved before.  The last
+        // batch's helper has exited or will after inverting the last published system: wait for it.
+        HIPCHK(hipStreamSynchronize(p->side));
+        HIPCHK(hipMemset(p->wsync, 0, 2 * sizeof(unsigned)));
+    }
     if (reset_iter) {
         p->h_state->iter = 0;
         p->h_state->change = 1.0;
@@ -480,9 +504,13 @@ int read_state(mcc_problem* p) {
 }
 
 int check_state_error(mcc_problem* p) {
-    if (p->h_state->error & 4) return fail(MCC_ECOMM, "peer exchange timed out (a rank did not deliver)");
-    if (p->h_state->error & 2) return fail(MCC_ENOTPD, "reduced camera system is not positive definite");
-    if (p->h_state->error & 1) return fail(MCC_ENOTPD, "a photo normal-equation block is not positive definite");
+    const int e = p->h_state->error;
+    if (e & mcc::kErrPeerTimeout) return fail(MCC_ECOMM, "peer exchange timed out (a rank did not deliver)");
+    if (e & mcc::kErrWarmTimeout)
+        return fail(MCC_ETIMEOUT, "the warm-solve helper did not deliver the previous step's inverse in time");
+    if (e & mcc::kErrCameraNotPD) return fail(MCC_ENOTPD, "reduced camera system is not positive definite");
+    if (e & mcc::kErrPhotoNotPD)
+        return fail(MCC_ENOTPD, "a photo normal-equation block is not positive definite (on this or another rank)");
     return MCC_OK;
 }
 
@@ -880,6 +908,14 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->warm = !p->fused && p->m > 30;
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
+    if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
+    if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
+    if (const char* f = std::getenv("MCC_FAULT_PHOTO")) p->fault_photo = std::atoi(f);
+    {
+        double peer_ms = 30000.0;   // the helper outlives a k_solve's longest wait at a peer exchange
+        if (const char* t = std::getenv("MCC_PEER_TIMEOUT_MS")) peer_ms = std::max(1.0, std::atof(t));
+        p->warm_idle_ticks = p->warm_wait_ticks + (long long)(peer_ms * 1e5) + 100000000LL;
+    }
     p->warm = p->warm && p->m <= 96;   // the staged system and inverse fit k_solve's LDS up to M = 96
     if (p->warm) {
         const size_t M = 16 * (size_t)((p->m + 15) / 16);

@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
         double2* L2 = reinterpret_cast<double2*>(sLi + 36 * q);
 #pragma unroll
         for (int k = 0; k < 18; ++k) L2[k] = make_double2(Li[(2 * k) / 6][(2 * k) % 6], Li[(2 * k + 1) / 6][(2 * k + 1) % 6]);
-        if (bad) atomicOr(&st->error, 1);
+        if (bad || photo == a.fault_photo) atomicOr(&st->error, kErrPhotoNotPD);
     }
     __syncthreads();
     SSTAMP(stp, 8, 0);

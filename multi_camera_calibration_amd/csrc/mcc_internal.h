@@ -19,11 +19,16 @@ struct State {
     double change;    // ||G|| / ||x|| of the last update
     double alpha;     // 0.95^(k+1) of the running step
     double cam_normG2, cam_normX2;   // global-block partials of the last update
-    int error;        // bit 0: photo block not PD, bit 1: camera system not PD, bit 2: peer timeout
+    int error;        // kErr* bits below
     int pending;      // a solved photo update waits to be applied by the next k_linearize
     unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
     long long xchg_ticks; // s_memrealtime ticks (100 MHz) inside peer exchanges, summed (monotonic)
 };
+// State::error bits
+constexpr int kErrPhotoNotPD = 1;    // a photo's 6 x 6 block (any rank: summed through the exchange)
+constexpr int kErrCameraNotPD = 2;   // the reduced camera system
+constexpr int kErrPeerTimeout = 4;   // a peer did not deliver its system
+constexpr int kErrWarmTimeout = 8;   // the warm-solve helper did not deliver the previous inverse
 
 // Peer transport (multi-GPU without RCCL in the step): every rank's final arriver writes its packed
 // reduced system straight into every peer's inbox over xGMI, then sums all ranks' systems in rank
@@ -105,6 +110,8 @@ struct LinArgs {
     const int* prep_ptr;     // [n_prep + 1] first photo of each group
     const int* prep_edge;    // [n_prep + 1] first edge of each group
     int n_prep, prep_lanes;  // prep_lanes: 4 (k_prep4) or 1 (k_prep, one lane per edge)
+    int fault_photo;         // test (MCC_FAULT_PHOTO): this local photo's 6 x 6 block is reported not
+                             // positive definite (its factor stays finite); -1 off
 };
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
@@ -219,14 +226,23 @@ struct SchurArgs {
 // when the refinement does not converge within kWarmMaxIters corrections.  sinv_ok_sys, sprev and
 // sync are uncached device memory (the helper and the k_solve launches hand them over while both
 // run); sinv is ordinary memory, written back by the helper (agent release) before its epoch.
+// Which algorithm a step takes depends only on the systems (the epoch count, the helper's PD flag,
+// the refinement's convergence), never on timing: k_solve always waits for the previous system's
+// inverse, and a helper that does not deliver within wait_ticks fails the step (error bit 3,
+// MCC_ETIMEOUT) instead of switching to the direct elimination.
 struct WarmCtx {
     double* sinv;            // [M x M] (M = 16 ceil(m / 16), row-major) the helper's inverse
     int* sinv_ok_sys;        // the helper's elimination found the system positive definite
     double* sprev;           // [packed [S | r] rounded up to even] the last solved system, for the helper
     unsigned* sync;          // [3] epochs: systems published by k_solve, systems inverted by the helper; stop
-    long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), helper late
+    long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), waited for the helper
     int poison;              // test (MCC_WARM_POISON=1): the helper publishes a NaN inverse, so every
                              // warm solve must fall back to the direct elimination
+    long long wait_ticks;    // k_solve's bound on the wait for the helper (s_memrealtime, 100 MHz)
+    long long idle_ticks;    // the helper exits after this long without a new system (a safety net: the
+                             // batch's k_solves publish or raise the stop flag, and the host launches the
+                             // helper only after the batch's graphs exist)
+    long long delay_ticks;   // test (MCC_WARM_DELAY_US): the helper holds each inverse back this long
 };
 constexpr int kWarmMaxIters = 4;
 

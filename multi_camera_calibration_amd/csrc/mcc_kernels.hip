@@ -876,11 +876,24 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
         st->epoch = ep;
         st->xchg_ticks += (long long)__builtin_amdgcn_s_memrealtime() - tx0;   // mcc_timing_exchange
         if (to_s) {
-            st->error |= 4;
+            st->error |= kErrPeerTimeout;
             st->done = 1;
         }
     }
     return !to_s;
+}
+
+// The stop-test norm slot w (0: normG2, 1: normX2) the final arriver writes into the packed system.
+// A photo block that was not positive definite on THIS rank (its workgroup set kErrPhotoNotPD before
+// its ticket) turns normX2 into a NaN: the exchange's sum (peer transport or RCCL) carries the NaN to
+// every rank, and every rank's solve_global stops on the same step with the same error, so the
+// ranks' replicated camera blocks never diverge (a rank-local stop would leave the other ranks
+// solving a system without its shard).  normX2 is a sum of squared float32 parameters, NaN only
+// when the state itself is, which is an error too.
+__device__ __forceinline__ double photo_flag_norm(State* st, int w, double v) {
+    if (w == 1 && (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kErrPhotoNotPD))
+        return __builtin_nan("");
+    return v;
 }
 
 template <bool LARGE>
@@ -1229,7 +1242,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             }
             z[lane] = zi;
         }
-        if (bad && lane == 0) atomicOr(&st->error, 1);
+        if ((bad || photo == a.fault_photo) && lane == 0) atomicOr(&st->error, kErrPhotoNotPD);
     }
     __syncthreads();
     STAMP(6);
@@ -1364,6 +1377,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             } else {
                 v = 0.0;
             }
+            v = photo_flag_norm(st, w, v);
         }
         if (!peer) place(t, v);
         a.packed[t] = v;
@@ -2132,7 +2146,7 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
         double2* L2 = reinterpret_cast<double2*>(sLi + 36 * q);
 #pragma unroll
         for (int k = 0; k < 18; ++k) L2[k] = make_double2(Li[(2 * k) / 6][(2 * k) % 6], Li[(2 * k + 1) / 6][(2 * k + 1) % 6]);
-        if (bad) atomicOr(&st->error, 1);
+        if (bad || photo == a.fault_photo) atomicOr(&st->error, kErrPhotoNotPD);
     }
     __syncthreads();
     SSTAMP(stp, 3, 0);
@@ -2630,7 +2644,10 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
 // stale copy): k_solve publishes S_t (sprev, then sync[0] = t's epoch, after its stores drained);
 // the helper inverts it into sinv and publishes sync[1] = that epoch; the next k_solve waits for
 // sync[1] == sync[0] before it reads sinv or overwrites sprev.  It always refines with exactly the
-// previous step's inverse, so the result does not depend on timing.
+// previous step's inverse, so the result does not depend on timing: there is no "helper late ->
+// direct elimination" switch (a helper that has not delivered after WarmCtx::wait_ticks fails the
+// step with kErrWarmTimeout), and on a sharded problem every rank takes the same branch on the same
+// bits (tests/test_warm_solve.py: a delayed helper, one rank delayed at world 2).
 // Thread t holds row i = t >> 2 of S_{t+1} and of S_t^-1, columns [24 g, 24 g + 24) (g = t & 3; zero
 // beyond m), in registers; a product A v is the quad's four partial dot products (v from LDS, six
 // 16-B reads in flight) added by two DPP quad permutes.  (Measured, not kept: 4 x 6 blocks per
@@ -2641,8 +2658,6 @@ __device__ __forceinline__ void gj_blocked(const double* packed, double* x, doub
 // costs none); otherwise (kWarmMaxIters corrections, a NaN) the direct elimination runs.
 constexpr int kWarmQ = 24;                 // M <= 96 (m <= 96): the staged S and S^-1 fit in LDS
 constexpr int kWarmN = 4 * kWarmQ;
-constexpr long long kWarmWaitTicks = 50000;        // k_solve waits <= 0.5 ms for the helper (100 MHz ticks)
-constexpr long long kHelperIdleTicks = 500000;     // the helper exits after 5 ms without a new system
 __device__ __forceinline__ double wave_max(double v) {
     {
         double a = v, b = v;
@@ -2825,8 +2840,8 @@ __device__ __forceinline__ void warm_stop(const WarmCtx& w) {
 //               a wait for the helper only if it has not inverted the last published system;
 //   warm_finish (after the stop test): stage [S | r] in LDS and publish it as sprev for the helper,
 //               load S_t^-1 (uncached) into LDS, refine; the direct elimination (gj_blocked) when
-//               there is no inverse yet, the helper is late, or the refinement does not converge;
-//               then the new epoch.  Barriers that only order LDS are raw s_barriers, so the sprev
+//               there is no inverse yet, the last system was not positive definite, or the
+//               refinement does not converge; then the new epoch.  Barriers that only order LDS are raw s_barriers, so the sprev
 //               stores drain behind the refinement instead of at each barrier.
 // x: LDS (the solution), followed by the work area (mcc_solve_shmem).
 constexpr int kWarmPer = 8;   // double2 of [S | r] per thread: one pass up to m = 90 (2 093 double2 at 512 threads)
@@ -2842,6 +2857,9 @@ __device__ __forceinline__ void warm_issue(const double* packed, int m, WarmStag
         ws.v[u] = q < n2 ? reinterpret_cast<const double2*>(packed)[q] : make_double2(0.0, 0.0);
     }
 }
+// use: 1 refine with the helper's inverse, 0 the direct elimination (no system inverted yet, or the
+// helper found the last one not positive definite -- both functions of the systems alone), -1 the
+// helper did not deliver within wait_ticks (the step fails: kErrWarmTimeout)
 __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigned* e_s) {
     const uint4 sy = *reinterpret_cast<const uint4*>(w.sync);   // {published, inverted, stop, PD}
     const unsigned e = sy.x;
@@ -2851,16 +2869,16 @@ __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigne
         w.stats[3] += 1;
     } else {
         if (h != e) {
+            w.stats[4] += 1;   // waited for the helper (the branch taken below does not depend on it)
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            while (h != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < kWarmWaitTicks) {
+            while (h != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < w.wait_ticks) {
                 __builtin_amdgcn_s_sleep(2);
                 h = ld_sys_u32(w.sync + 1);
             }
             ok = ld_sys_u32(w.sync + 3);
         }
-        use = h == e && ok;
-        if (h != e) w.stats[4] += 1;   // the helper is late: direct elimination
-        else if (!use) w.stats[3] += 1;
+        use = h != e ? -1 : ok ? 1 : 0;
+        if (use == 0) w.stats[3] += 1;
     }
     *use_s = use;
     *e_s = e;
@@ -2880,7 +2898,7 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
         }
     }
     bool solved = false;
-    if (use) {
+    if (use > 0) {
         // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
         // rows of S_{t+1} from the staged packed system; then S_t^-1 into LDS, rows padded to
         // M + 2 (16 rows of a wave would otherwise share banks)
@@ -2974,7 +2992,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
             unsigned e = ld_sys_u32(w.sync);
             int quit = 0;
             while (e == seen) {
-                if (ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - t0 > kHelperIdleTicks) {
+                if (ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - t0 > w.idle_ticks) {
                     quit = 1;
                     break;
                 }
@@ -3019,6 +3037,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tid == 0 && w.delay_ticks > 0) {   // test: a slow helper (k_solve must wait, not switch)
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < w.delay_ticks) __builtin_amdgcn_s_sleep(8);
+        }
         if (tid == 0) st_sys_u32(w.sync + 1, e);
         seen = e;
     }
@@ -3051,8 +3073,11 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     if (wrm && tid == 64) warm_check(*warm, &s_use, &s_ep);
     if (tid == 0) {
         // the error bits the step's photo work set (bit 0), read with the state so that the stop
-        // at the end needs no further round trip
+        // at the end needs no further round trip.  On a sharded problem a photo block that is not
+        // positive definite on ANY rank arrives here as a NaN in the summed normX2 slot
+        // (photo_flag_norm): every rank then stops on the same step with the same error
         s_err0 = __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(normX2 == normX2)) s_err0 |= kErrPhotoNotPD;
         s_bad = 0;
         const int k = st->iter;
         double change = 1.0;
@@ -3084,6 +3109,14 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     __syncthreads();
     if (stop) {
         if (warm) warm_stop(*warm);
+        return;
+    }
+    if (wrm && s_use < 0) {   // the helper did not deliver: fail the step rather than switch algorithms
+        if (tid == 0) {
+            atomicOr(&st->error, kErrWarmTimeout);
+            st->done = 1;
+        }
+        warm_stop(*warm);
         return;
     }
     SSTAMP(a.stamps, 4, 0);
@@ -3126,6 +3159,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     // no launch in flight loses a workgroup's ticket
     __syncthreads();
     if (tid == 0 && ((s_err0 & 3) || s_bad || (!LARGE && s_bad_rows))) {
+        if (s_err0 & kErrPhotoNotPD) atomicOr(&st->error, kErrPhotoNotPD);   // another rank's photo
         st->done = 1;
         if (warm) warm_stop(*warm);
     }
@@ -3261,6 +3295,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         }
         if (a.rank == 0) v += cn;
         if (iter <= 0) v = 0.0;
+        v = photo_flag_norm(st, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
     }

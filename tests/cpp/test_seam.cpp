@@ -6,8 +6,9 @@
 //
 //   test_seam selftest              host only (no GPU): the cv::Mat shim, conjungate (public,
 //                                   multicalib.hpp:157) against a direct solve, compose_motion's
-//                                   partials against central differences, the per-edge Jacobian's
-//                                   loud default, and that the subclasses construct
+//                                   partials against central differences, the per-edge Jacobian
+//                                   (shapes, the FRONT / BACK / DoubleSide block structure), and
+//                                   that the subclasses construct
 //   test_seam strict                strict-reference mode: an edge whose stored transform fails
 //                                   isValidPose aborts optimizeExtrinsics (src/mymulticalib.cpp:706)
 //   test_seam run <in.bin>          (GPU) a fixture problem (tests/cpp blob, see test_multicalib.cpp)
@@ -15,6 +16,12 @@
 //                                   counting subclass (the reference's host loop through the
 //                                   overridden virtuals): same iterations, parameters, error; the
 //                                   overrides called where the reference calls them
+//   test_seam refstyle <in.bin>     (GPU) a subclass whose computeJacobianExtrinsic is the
+//                                   reference's body (src/mymulticalib.cpp:668-818,
+//                                   src/doubleSide.cpp:434-581): the dense J assembled edge by edge
+//                                   from computePhotoCameraJacobian, J^T J, J^T E, conjungate -- all
+//                                   on the host -- against the library's GPU linearisation (deltaX,
+//                                   JTE) and, through the reference's host loop, its device loop
 #include "opencv2/ccalib/doubleSide.hpp"
 
 #include <cstdio>
@@ -22,6 +29,7 @@
 #include <fstream>
 #include <memory>
 #include <random>
+#include <type_traits>
 
 static int g_fail = 0;
 #define EXPECT(c)                                                              \
@@ -45,9 +53,11 @@ public:
         out.assign(10, Mat());
         compose_motion(om1, T1, om2, T2, out[0], out[1], out[2], out[3], out[4], out[5], out[6], out[7], out[8], out[9]);
     }
-    void baseEdgeJacobian() {
-        Mat m, e;
-        MyMultiCameraCalibration::computePhotoCameraJacobian(0, m, m, m, m, m, m, e, e, m, m, m, m, m, e, e, e);
+    void edgeJacobian(int side, const Mat& rP, const Mat& tP, const Mat& rC, const Mat& tC, const Mat& rD, const Mat& tD,
+                      Mat& rt, Mat& tt, const Mat& obj, const Mat& img, const Mat& K, const Mat& D, const Mat& xi,
+                      Mat& jp, Mat& jc, Mat& e) {
+        MyMultiCameraCalibration::computePhotoCameraJacobian(side, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jp,
+                                                             jc, e);
     }
 
 protected:
@@ -85,6 +95,12 @@ class CountingDoubleSide : public cv::multicalib::DoubleSideCalibration {
 public:
     using DoubleSideCalibration::DoubleSideCalibration;
     Calls calls;
+    void edgeJacobian(int side, const Mat& rP, const Mat& tP, const Mat& rC, const Mat& tC, const Mat& rD, const Mat& tD,
+                      Mat& rt, Mat& tt, const Mat& obj, const Mat& img, const Mat& K, const Mat& D, const Mat& xi,
+                      Mat& jp, Mat& jg, Mat& e) {
+        DoubleSideCalibration::computePhotoCameraJacobian(side, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jp,
+                                                          jg, e);
+    }
 
 protected:
     virtual void computeJacobianExtrinsic(const Mat& extrinsicParams, Mat& JTJ_inv, Mat& JTE, Mat& deltaX) override {
@@ -109,6 +125,100 @@ class PublicConjungate : public cv::multicalib::MultiCameraCalibration {
 public:
     using MultiCameraCalibration::MultiCameraCalibration;
 };
+
+// computeJacobianExtrinsic written as the reference writes it (src/mymulticalib.cpp:668-818 for
+// MyMulti, src/doubleSide.cpp:434-581 for DoubleSide): per edge, slice the photo and camera (or ds)
+// parameters, call the per-edge computePhotoCameraJacobian, copy its blocks into the dense J and E;
+// then JTJ = J^T J, JTE = J^T E, deltaX = conjungate(JTJ, JTE).  Everything on the host: the per-edge
+// Jacobian is the build's host restatement, the product and the solve the cv::Mat shim's.
+template <class Base>
+class RefStyle : public Base {
+public:
+    using Base::Base;
+    int edgeCalls = 0;
+    void jacobianAt(const Mat& x, Mat& JTE, Mat& deltaX) {
+        Mat jinv;
+        this->computeJacobianExtrinsic(x, jinv, JTE, deltaX);
+    }
+    void libraryJacobianAt(const Mat& x, Mat& JTE, Mat& deltaX) {   // the GPU linearisation (the seam's default)
+        Mat jinv;
+        Base::computeJacobianExtrinsic(x, jinv, JTE, deltaX);
+    }
+    Mat params() { return this->buildParas(); }
+
+protected:
+    static constexpr bool kDoubleSide = std::is_base_of<cv::multicalib::DoubleSideCalibration, Base>::value ||
+                                        std::is_same<cv::multicalib::DoubleSideCalibration, Base>::value;
+    void computePhotoCameraJacobian(int patternSide, const Mat& rvecPhoto, const Mat& tvecPhoto, const Mat& rvecCamera,
+                                    const Mat& tvecCamera, const Mat& rvecDoubleside, const Mat& tvecDoubleside,
+                                    Mat& rvecTran, Mat& tvecTran, const Mat& objectPoints, const Mat& imagePoints,
+                                    const Mat& K, const Mat& distort, const Mat& xi, Mat& jacobianPhoto,
+                                    Mat& jacobianGlobal, Mat& E) override {
+        ++edgeCalls;
+        Base::computePhotoCameraJacobian(patternSide, rvecPhoto, tvecPhoto, rvecCamera, tvecCamera, rvecDoubleside,
+                                         tvecDoubleside, rvecTran, tvecTran, objectPoints, imagePoints, K, distort, xi,
+                                         jacobianPhoto, jacobianGlobal, E);
+    }
+    void computeJacobianExtrinsic(const Mat& extrinsicParams, Mat& JTJ_inv, Mat& JTE, Mat& deltaX) override {
+        const int nParam = (int)extrinsicParams.total();
+        const int nEdge = (int)this->_edgeList.size();
+        std::vector<int> pointsLocation(nEdge + 1, 0);
+        for (int edgeIdx = 0; edgeIdx < nEdge; ++edgeIdx) {
+            const int nPoints = this->objectPointsMat(this->_edgeList[edgeIdx].cameraVertex, this->_edgeList[edgeIdx].photoIndex).rows;
+            pointsLocation[edgeIdx + 1] = pointsLocation[edgeIdx] + nPoints * 2;
+        }
+        JTJ_inv = Mat();
+        Mat J = Mat::zeros(pointsLocation[nEdge], nParam, CV_64F);
+        Mat E = Mat::zeros(pointsLocation[nEdge], 1, CV_64F);
+        Mat RvecDoubleSide, TvecDoubleSide;
+        if constexpr (kDoubleSide) {   // the global block is the first six parameters (doubleSide.cpp:450-451)
+            RvecDoubleSide = extrinsicParams.colRange(0, 3);
+            TvecDoubleSide = extrinsicParams.colRange(3, 6);
+        } else {
+            RvecDoubleSide = this->doubleSideTransform_rvec();
+            TvecDoubleSide = this->doubleSideTransform_tvec();
+        }
+        for (int edgeIdx = 0; edgeIdx < nEdge; ++edgeIdx) {
+            const auto& eg = this->_edgeList[edgeIdx];
+            const int photoVertex = eg.photoVertex, photoIndex = eg.photoIndex, cameraVertex = eg.cameraVertex;
+            const Mat objectPoints = this->objectPointsMat(cameraVertex, photoIndex);
+            const Mat imagePoints = this->imagePointsMat(cameraVertex, photoIndex);
+            const int paraRow = kDoubleSide ? photoVertex - this->_nCamera + 1 : photoVertex - 1;
+            const Mat RvecPhoto = extrinsicParams.colRange(paraRow * 6, paraRow * 6 + 3);
+            const Mat TvecPhoto = extrinsicParams.colRange(paraRow * 6 + 3, paraRow * 6 + 6);
+            Mat RvecCamera, TvecCamera;
+            if constexpr (kDoubleSide) {
+                RvecCamera = this->camerasPose_rvec(cameraVertex);
+                TvecCamera = this->camerasPose_tvec(cameraVertex);
+            } else if (cameraVertex > 0) {
+                RvecCamera = extrinsicParams.colRange((cameraVertex - 1) * 6, (cameraVertex - 1) * 6 + 3);
+                TvecCamera = extrinsicParams.colRange((cameraVertex - 1) * 6 + 3, (cameraVertex - 1) * 6 + 6);
+            } else {
+                RvecCamera = Mat::zeros(3, 1, CV_32F);
+                TvecCamera = Mat::zeros(3, 1, CV_32F);
+            }
+            Mat Rvectran, Tvectran, jacobianPhoto, jacobianGlobal, error;
+            computePhotoCameraJacobian(eg.patternSide, RvecPhoto, TvecPhoto, RvecCamera, TvecCamera, RvecDoubleSide,
+                                       TvecDoubleSide, Rvectran, Tvectran, objectPoints, imagePoints,
+                                       this->cameraMatrixMat(cameraVertex), this->distortCoeffsMat(cameraVertex),
+                                       this->xiMat(cameraVertex), jacobianPhoto, jacobianGlobal, error);
+            const int rowBegin = pointsLocation[edgeIdx], rowEnd = pointsLocation[edgeIdx + 1];
+            if constexpr (kDoubleSide) {
+                jacobianGlobal.copyTo(J.rowRange(rowBegin, rowEnd).colRange(0, 6));
+            } else if (cameraVertex > 0) {
+                jacobianGlobal.copyTo(J.rowRange(rowBegin, rowEnd).colRange((cameraVertex - 1) * 6, cameraVertex * 6));
+            }
+            jacobianPhoto.copyTo(J.rowRange(rowBegin, rowEnd).colRange(paraRow * 6, (paraRow + 1) * 6));
+            error.copyTo(E.rowRange(rowBegin, rowEnd));
+        }
+        const Mat Jt = J.t();
+        const Mat JTJ = Jt * J;
+        JTE = Jt * E;
+        deltaX = this->conjungate(JTJ, JTE);
+    }
+};
+using RefMyMulti = RefStyle<cv::multicalib::MyMultiCameraCalibration>;
+using RefDoubleSide = RefStyle<cv::multicalib::DoubleSideCalibration>;
 
 static Mat vec3m(double a, double b, double c) {
     Mat m(3, 1, CV_64F);
@@ -197,17 +307,44 @@ static int selftest() {
             }
         EXPECT(worst < 1e-6);
     }
-    // ---- the per-edge CPU Jacobian is not part of this build: the base version fails loudly
+    // ---- the per-edge Jacobian (computePhotoCameraJacobian): shapes, and the block structure of
+    // MyMulti's FRONT / BACK chains and DoubleSide's zero ds block for FRONT views
     {
         CountingMyMulti mc(2);
-        bool threw = false;
-        try {
-            mc.baseEdgeJacobian();
-        } catch (const std::logic_error&) {
-            threw = true;
+        Mat obj(4, 3, CV_32F), img(4, 2, CV_32F), K = Mat::zeros(3, 3, CV_32F), D = Mat::zeros(1, 5, CV_32F), xi;
+        for (int i = 0; i < 4; ++i) {
+            obj.at<float>(i, 0) = 40.f * (i % 2);
+            obj.at<float>(i, 1) = 40.f * (i / 2);
+            obj.at<float>(i, 2) = 0.f;
+            img.at<float>(i, 0) = 900.f + 10.f * i;
+            img.at<float>(i, 1) = 500.f;
         }
-        EXPECT(threw);
+        K.at<float>(0, 0) = K.at<float>(1, 1) = 1200.f;
+        K.at<float>(0, 2) = 960.f;
+        K.at<float>(1, 2) = 540.f;
+        K.at<float>(2, 2) = 1.f;
+        D.at<float>(0, 0) = -0.1f;
+        const Mat rP = vec3m(0.3, -0.2, 0.1), tP = vec3m(-20, 10, 1200), rC = vec3m(0.05, 0.2, -0.1),
+                  tC = vec3m(-300, 5, 40), rD = vec3m(0.0, 3.1, 0.0), tD = vec3m(10, 0, -25);
+        Mat jpF, jcF, eF, jpB, jcB, eB, rt, tt;
+        mc.edgeJacobian(0, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jpF, jcF, eF);
+        mc.edgeJacobian(1, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jpB, jcB, eB);
+        EXPECT(jpF.rows == 8 && jpF.cols == 6 && jcF.rows == 8 && eF.rows == 8 && eF.cols == 1 && eF.type() == CV_64F);
+        EXPECT(rt.empty() && tt.empty());   // MyMulti leaves Rvectran / Tvectran alone
+        bool finite = true;
+        for (int r = 0; r < 8; ++r) {
+            finite = finite && std::isfinite(eF.at<double>(r)) && std::isfinite(eB.at<double>(r));
+            for (int c = 0; c < 6; ++c)
+                finite = finite && std::isfinite(jpF.at<double>(r, c)) && std::isfinite(jcB.at<double>(r, c));
+        }
+        EXPECT(finite);
+        EXPECT(cv::norm(eF - eB) > 1.0);   // the BACK pose differs by the double-side transform
         CountingDoubleSide ds(2);
+        Mat jp2, jg2, e2;
+        ds.edgeJacobian(0, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jp2, jg2, e2);
+        EXPECT(cv::norm(jg2) == 0.0 && cv::norm(jp2 - jpF) == 0.0 && cv::norm(e2 - eF) == 0.0);
+        ds.edgeJacobian(1, rP, tP, rC, tC, rD, tD, rt, tt, obj, img, K, D, xi, jp2, jg2, e2);
+        EXPECT(cv::norm(jg2) > 0.0 && cv::norm(jp2 - jpB) == 0.0 && cv::norm(e2 - eB) == 0.0);
         EXPECT(ds.calls.jac == 0);
     }
     std::printf("selftest %s (%d failures)\n", g_fail ? "FAILED" : "ok", g_fail);
@@ -350,15 +487,79 @@ static int run(const char* in) {
     return rc;
 }
 
+// the reference-style subclass against the library: its host linearisation at x0 against the GPU's
+// (deltaX within 1e-6, JTE within 1e-9 of the largest entry), then its host loop (one host
+// linearisation per step) against the library class's device loop
+template <class Ref, class Lib>
+static int refstyle_compare(const Blob& b, Lib& lib, Ref& ref) {
+    fill(lib, b);
+    fill(ref, b);
+    const Mat x0 = ref.params();
+    Mat jte_h, dx_h, jte_g, dx_g;
+    ref.jacobianAt(x0, jte_h, dx_h);
+    const int nEdgeCalls = ref.edgeCalls;
+    ref.libraryJacobianAt(x0, jte_g, dx_g);
+    double jmax = 0, dmax = 0, jdiff = 0, ddiff = 0;
+    for (int i = 0; i < dx_h.rows; ++i) {
+        jmax = std::max(jmax, std::fabs(jte_g.at<double>(i)));
+        dmax = std::max(dmax, std::fabs(dx_g.at<double>(i)));
+        jdiff = std::max(jdiff, std::fabs(jte_h.at<double>(i) - jte_g.at<double>(i)));
+        ddiff = std::max(ddiff, std::fabs(dx_h.at<double>(i) - dx_g.at<double>(i)));
+    }
+    std::printf("refstyle: %d edges, JTE diff %.3g of %.3g, deltaX diff %.3g of %.3g\n", nEdgeCalls, jdiff, jmax, ddiff, dmax);
+    EXPECT(nEdgeCalls == (int)ref._edgeList.size());
+    EXPECT(jdiff <= 1e-9 * jmax);
+    EXPECT(ddiff <= 1e-6 * dmax);
+    const double e_lib = lib.optimizeExtrinsics();
+    const double e_ref = ref.optimizeExtrinsics();
+    const std::vector<float> x_lib = lib.buildParaVector(), x_ref = ref.buildParaVector();
+    long long worst = 0;
+    for (size_t i = 0; i < x_lib.size(); ++i) worst = std::max(worst, ulp_diff(x_lib[i], x_ref[i]));
+    std::printf("refstyle loop: library %d iterations, error %.12g; host %d iterations, error %.12g; max %lld ulp\n",
+                lib.iterations(), e_lib, ref.iterations(), e_ref, worst);
+    EXPECT(lib.iterations() == ref.iterations());
+    EXPECT(std::fabs(e_lib - e_ref) <= 1e-6);
+    EXPECT(worst <= 1);
+    return g_fail ? 1 : 0;
+}
+
+static int refstyle(const char* in) {
+    const Blob b = read_blob(in);
+    const mcc::multicalib::TermCriteria crit(b.crit_type, b.crit_max, b.eps);
+    int rc = 0;
+    if (b.model == MCC_MODEL_PINHOLE) {
+        cv::multicalib::MyMultiCameraCalibration lib(b.C, crit);
+        RefMyMulti ref(b.C, crit);
+        if (b.has_ds) {
+            std::copy(b.dsp.begin(), b.dsp.end(), lib.doubleSideTransform.begin());
+            std::copy(b.dsp.begin(), b.dsp.end(), ref.doubleSideTransform.begin());
+        }
+        rc = refstyle_compare(b, lib, ref);
+    } else if (b.model == MCC_MODEL_DOUBLESIDE) {
+        cv::multicalib::DoubleSideCalibration lib(b.C, crit);
+        RefDoubleSide ref(b.C, crit);
+        for (int c = 0; c < b.C; ++c) {
+            std::copy(b.cp.begin() + 16 * c, b.cp.begin() + 16 * (c + 1), lib.camerasPose[c].begin());
+            std::copy(b.cp.begin() + 16 * c, b.cp.begin() + 16 * (c + 1), ref.camerasPose[c].begin());
+        }
+        rc = refstyle_compare(b, lib, ref);
+    } else {
+        std::printf("refstyle: omnidirectional fixture skipped (the MyMulti / DoubleSide bodies)\n");
+    }
+    std::printf("refstyle %s\n", rc ? "FAILED" : "ok");
+    return rc;
+}
+
 int main(int argc, char** argv) {
     try {
         if (argc >= 2 && !std::strcmp(argv[1], "selftest")) return selftest();
         if (argc >= 2 && !std::strcmp(argv[1], "strict")) return strict();
         if (argc >= 3 && !std::strcmp(argv[1], "run")) return run(argv[2]);
+        if (argc >= 3 && !std::strcmp(argv[1], "refstyle")) return refstyle(argv[2]);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 2;
     }
-    std::fprintf(stderr, "usage: test_seam selftest | strict | run <in.bin>\n");
+    std::fprintf(stderr, "usage: test_seam selftest | strict | run <in.bin> | refstyle <in.bin>\n");
     return 2;
 }

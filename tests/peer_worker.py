@@ -45,6 +45,18 @@ def shard(case, world, rank):
     return p, mine, rig.subset_photos(p, mine)
 
 
+def fault_run(ba, q, eps):
+    """A shard whose photo block is reported not positive definite (MCC_FAULT_PHOTO on one rank):
+    every rank's optimize must fail with MCC_ENOTPD on the same step, and the replicated camera
+    block must stay bit-identical (the flag travels in the exchanged system)."""
+    try:
+        ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=eps)
+        err = ""
+    except api.MccError as e:
+        err = str(e)
+    return err
+
+
 def main():
     case, rank, world, rdv, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4], sys.argv[5]
     steps = int(sys.argv[6]) if len(sys.argv) > 6 else 100
@@ -55,6 +67,12 @@ def main():
     handles = api.file_allgather(os.path.join(rdv, "handles"), rank, world, ba.peer_handle())
     ba.peer_init(handles, world, rank)
     mx = ba.allreduce_max(rank + 0.5)
+    if os.environ.get("MCC_PEER_WORKER_MODE") == "fault":
+        err = fault_run(ba, q, float(sys.argv[7]) if len(sys.argv) > 7 else 1e-7)
+        x = ba.get_params()
+        ba.close()
+        np.savez(out, mine=mine, x=x, err=err, mx=mx)
+        return
     d, j = ba.compute_jacobian_extrinsic(q.x0)
     eps = float(sys.argv[7]) if len(sys.argv) > 7 else 1e-7   # the TermCriteria eps the test compares at
     x, _, it, ch = ba.optimize_extrinsics(q.x0, crit_type=3, max_count=200, eps=eps)

@@ -1,0 +1,124 @@
+"""The host per-edge Jacobian (mcc::multicalib::edgeJacobian, libmcc_host.so; C entry
+mcc_host_edge_jacobian) that the cv::Mat seam's computePhotoCameraJacobian runs -- the reference's
+per-edge linearisation for subclasses that assemble J edge by edge the way the reference's
+computeJacobianExtrinsic does:
+
+    base class   src/multicalib.cpp:717-824      (the omnidirectional fixtures)
+    MyMulti      src/mymulticalib.cpp:468-614    (pinhole; BACK views, hazard A12)
+    DoubleSide   src/doubleSide.cpp:288-430      (ds block, zero for FRONT views)
+
+Checked on CPU against the oracle's restatement of the same function (ora_edge_linearize, which
+follows OpenCV's 3 x 9 Rodrigues / matMulDeriv chains) on every edge of every golden fixture:
+the float32 residuals bit for bit (up to rare 1-ulp FP64 ties), the Jacobians to 1e-8 of each row's
+largest entry (closed-form SO(3) chains against OpenCV's numerical 3 x 9 ones; the BACK chain goes
+through the double-side transform's rotation of ~pi, where both forms lose digits to sin(theta) ~ 0:
+2.6e-9 there, 1e-11 elsewhere).  Parity of the oracle itself: tests/test_oracle_math.py.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from multi_camera_calibration_amd import api, rig
+from oracle import oracle_py as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURES = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "*.npz")))
+
+_d = ctypes.POINTER(ctypes.c_double)
+_f = ctypes.POINTER(ctypes.c_float)
+
+
+@pytest.fixture(scope="module")
+def host():
+    api.build()
+    api.lib()   # libmcc.so first (libmcc_host.so links it)
+    L = ctypes.CDLL(api.HOST_LIB_PATH)
+    L.mcc_host_edge_jacobian.argtypes = [ctypes.c_int] * 3 + [_d] * 6 + [ctypes.c_int, _f, _f, _f, _f, ctypes.c_int,
+                                                                         ctypes.c_float, _d, _d, _d, _f]
+    return L
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def _edge_inputs(p, x, e):
+    """The per-edge arguments as the reference's computeJacobianExtrinsic slices them."""
+    cam, photo, side = int(p.edge_cam[e]), int(p.edge_photo[e]), int(p.edge_side[e]) if p.edge_side is not None else 0
+    c = int(p.photo_col(photo))
+    rP, tP = x[c:c + 3].astype(np.float64), x[c + 3:c + 6].astype(np.float64)
+    rD = tD = None
+    if p.model == rig.DOUBLESIDE:
+        P4 = np.asarray(p.cam_pose, np.float32).reshape(-1, 4, 4)[cam]
+        r, _ = O.rodrigues_m2v(P4[:3, :3].astype(np.float64))
+        rC = r.astype(np.float32).astype(np.float64)   # cameraPose2vec: Rodrigues of the CV_32F pose
+        tC = P4[:3, 3].astype(np.float64)
+        rD, tD = x[0:3].astype(np.float64), x[3:6].astype(np.float64)
+        cls = 2
+    else:
+        if cam == 0:
+            rC, tC = np.zeros(3), np.zeros(3)
+        else:
+            rC, tC = x[6 * (cam - 1):6 * (cam - 1) + 3].astype(np.float64), x[6 * (cam - 1) + 3:6 * cam].astype(np.float64)
+        if p.ds_pose is not None and p.model == rig.PINHOLE:
+            M = np.asarray(p.ds_pose, np.float64).reshape(4, 4)
+            rD, _ = O.rodrigues_m2v(M[:3, :3])
+            tD = M[:3, 3].copy()
+        cls = 0 if p.model == rig.OMNI else 1
+    return cls, side, rP, tP, rC, tC, rD, tD
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda f: os.path.splitext(os.path.basename(f))[0])
+def test_edge_jacobian_matches_oracle(host, path):
+    gd = dict(np.load(path))
+    p = rig.problem_from_arrays(gd)
+    x = np.asarray(gd["x0"], np.float32)
+    o = O.Oracle(p)
+    K = np.asarray(p.K, np.float32).reshape(-1, 9)
+    D = np.asarray(p.D, np.float32).reshape(p.n_cams, -1)
+    xi = np.asarray(p.xi, np.float32) if p.xi is not None else np.zeros(p.n_cams, np.float32)
+    nd = D.shape[1]
+    obj = np.asarray(p.obj, np.float32).reshape(-1, 3)
+    img = np.asarray(p.img, np.float32).reshape(-1, 2)
+    ties = total = 0
+    for e in range(p.n_edges):
+        cls, side, rP, tP, rC, tC, rD, tD = _edge_inputs(p, x, e)
+        cam, n, off = int(p.edge_cam[e]), int(p.edge_n[e]), int(p.edge_off[e])
+        jp = np.zeros((2 * n, 6)); jg = np.zeros((2 * n, 6)); E = np.zeros(2 * n); pose = np.zeros(6, np.float32)
+        ob = np.ascontiguousarray(obj[off:off + n]); im = np.ascontiguousarray(img[off:off + n])
+        kc = np.ascontiguousarray(K[cam]); dc = np.ascontiguousarray(D[cam])
+        rc = host.mcc_host_edge_jacobian(cls, int(p.model == rig.OMNI), side, _ptr(rP, _d), _ptr(tP, _d), _ptr(rC, _d),
+                                         _ptr(tC, _d), _ptr(rD, _d), _ptr(tD, _d), n, _ptr(ob, _f), _ptr(im, _f),
+                                         _ptr(kc, _f), _ptr(dc, _f), nd, float(xi[cam]), _ptr(jp, _d), _ptr(jg, _d),
+                                         _ptr(E, _d), _ptr(pose, _f))
+        assert rc == 0, (path, e)
+        jc_o, jp_o, E_o, _ = o.edge_linearize(x, e)
+        # residuals: float32 values, equal up to a 1-ulp FP64 tie of a transcendental
+        diff = E.astype(np.float32) != E_o.astype(np.float32)
+        ties += int(diff.sum())
+        total += E.size
+        if diff.any():
+            ulp = np.abs(E - E_o) / np.spacing(np.abs(E_o).astype(np.float32)).astype(np.float64)
+            assert ulp.max() <= 1.0, (path, e, ulp.max())
+        for a, b in ((jp, jp_o), (jg, jc_o)):
+            scale = np.maximum(np.abs(b).max(axis=1, keepdims=True), 1e-300)
+            assert (np.abs(a - b) / scale).max() <= 1e-8, (path, e, (np.abs(a - b) / scale).max())
+    assert ties <= max(2, 1e-4 * total), (ties, total)
+
+
+def test_edge_jacobian_rejects_bad_arguments(host):
+    z = np.zeros(3)
+    obj = np.zeros((1, 3), np.float32); img = np.zeros((1, 2), np.float32)
+    K = np.eye(3, dtype=np.float32).reshape(9); D = np.zeros(6, np.float32)
+    # nd = 6 is not an OpenCV distortion size; a BACK view without the double-side transform
+    assert host.mcc_host_edge_jacobian(1, 0, 0, *[_ptr(z, _d)] * 4, None, None, 1, _ptr(obj, _f), _ptr(img, _f),
+                                       _ptr(K, _f), _ptr(D, _f), 6, 0.0, None, None, None, None) == api_EINVAL()
+    assert host.mcc_host_edge_jacobian(1, 0, 1, *[_ptr(z, _d)] * 4, None, None, 1, _ptr(obj, _f), _ptr(img, _f),
+                                       _ptr(K, _f), _ptr(D, _f), 5, 0.0, None, None, None, None) == api_EINVAL()
+
+
+def api_EINVAL():
+    return -1   # MCC_EINVAL (include/mcc.h)

@@ -42,10 +42,11 @@ def test_file_allgather(tmp_path):
     assert out == [b"abc"]
 
 
-def _run_ranks(case, world, tmp_path, steps=100, eps=1e-7):
-    env = dict(os.environ, MCC_PEER_TIMEOUT_MS="20000")
+def _run_ranks(case, world, tmp_path, steps=100, eps=1e-7, rank_env=None, env_all=None):
+    """rank_env: {rank: {VAR: value}} for one rank's process only (a delayed helper, a fault)."""
     procs = []
     for r in range(world):
+        env = dict(os.environ, MCC_PEER_TIMEOUT_MS="20000", **(env_all or {}), **((rank_env or {}).get(r, {})))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "peer_worker.py"), case, str(r),
                                        str(world), str(tmp_path / "rdv"), str(tmp_path / f"r{r}.npz"), str(steps), repr(eps)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
@@ -130,3 +131,52 @@ def test_peer_ranks_one_device(case, world, tmp_path):
     else:
         assert ulp.max() <= 1, (case, world, int(ulp.max()), int((ulp > 0).sum()))
     print(f"{case}: {world} ranks on one device, {float(outs[0]['ms']):.4f} ms/step")
+
+
+@pytest.mark.gpu
+def test_warm_helper_delayed_on_one_rank(tmp_path):
+    """The m > 30 warm solve at world 2 with rank 1's helper holding every
+    inverse back by 3 ms (MCC_WARM_DELAY_US; the round-3 k_solve gave up after 0.5 ms and switched
+    that rank to the direct elimination).  Every rank solves the same bits by the same algorithm:
+    the global block is bit-identical on both ranks and bit-identical to the undelayed run, and the
+    oracle bars of test_peer_ranks_one_device hold (src/multicalib.cpp:462-514, the solve it
+    replaces :565-592)."""
+    case = "config3_small"
+    p = peer_worker.CASES[case]()
+    m = p.global_dim
+    (tmp_path / "base").mkdir()
+    (tmp_path / "slow").mkdir()
+    base = _run_ranks(case, 2, tmp_path / "base", steps=20)
+    slow = _run_ranks(case, 2, tmp_path / "slow", steps=20, rank_env={1: {"MCC_WARM_DELAY_US": "3000"}})
+    x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    for r in slow:
+        assert int(r["it"]) == it_ref
+    assert np.array_equal(slow[0]["x"][:m], slow[1]["x"][:m])
+    for a, b in zip(base, slow):
+        assert np.array_equal(a["x"], b["x"]) and int(a["it"]) == int(b["it"])
+    x = np.zeros_like(x_ref)
+    x[:m] = slow[0]["x"][:m]
+    for r in slow:
+        for k, ph in enumerate(r["mine"]):
+            c = p.photo_col(int(ph))
+            x[c:c + 6] = r["x"][m + 6 * k:m + 6 * k + 6]
+    _, mean = O.Oracle(p).project_error(x)
+    assert abs(mean - m_ref) <= 1e-6
+    assert f32_ulp_diff(x, x_ref).max() <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["config2_small", "config4_split", "config3_small"])
+def test_photo_not_pd_on_one_rank(case, tmp_path):
+    """A photo block that is not positive definite on ONE rank (MCC_FAULT_PHOTO=0 in rank 1's
+    process: the block's factor stays finite, the kind of failure a rank-local stop would hide from
+    its peers) fails every rank's optimize with MCC_ENOTPD, and the replicated global block stays
+    bit-identical: the flag rides in the exchanged system (the fused kernel's, k_schur's and
+    k_solve's exchanges)."""
+    p = peer_worker.CASES[case]()
+    outs = _run_ranks(case, 2, tmp_path, eps=_eps(case, p), env_all={"MCC_PEER_WORKER_MODE": "fault"},
+                      rank_env={1: {"MCC_FAULT_PHOTO": "0"}})
+    for r in outs:
+        assert "(-3)" in str(r["err"]) and "positive definite" in str(r["err"]), str(r["err"])
+    m = p.global_dim
+    assert np.array_equal(outs[0]["x"][:m], outs[1]["x"][:m])
