@@ -125,6 +125,12 @@ int mcc_check(mcc_problem *p);
 
 /* computeProjectError(x): edge_err[E] (reference edge order, may be NULL), mean. */
 int mcc_project_error(mcc_problem *p, const float *x, float *edge_err, double *mean);
+/* the same with the quantities the reference prints (src/mymulticalib.cpp:898-937): each corner's
+ * float32 L2 error corner_err[corners] (reference corner order: errorsVector, for the standard
+ * deviation), totalError (the float32 sum of the per-edge sums in edge order) and totalNPoints
+ * (2N per pinhole edge, N per omnidirectional one); every output may be NULL. */
+int mcc_project_error_detail(mcc_problem *p, const float *x, float *edge_err, float *corner_err,
+                             float *total_error, long long *total_points, double *mean);
 
 /* ---- multi-GPU (RCCL over xGMI).  All ranks hold the same cameras and disjoint photo sets;
  * x of a rank is [global block, its photos].  The global block stays identical on all ranks. */

@@ -30,6 +30,7 @@
 #ifndef MCC_MULTICALIB_HPP
 #define MCC_MULTICALIB_HPP
 
+#include <algorithm>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -235,7 +236,7 @@ public:
     // computeProjectError and paras2vertex; returns the reference's meanReProjError (also kept
     // in _error for writeParameters)
     double optimizeExtrinsics() {
-        if (strictReference) return optimizeExtrinsicsChecked();
+        if (strictReference || verboseOn()) return optimizeExtrinsicsChecked();
         std::vector<float> x = buildParaVector();
         check(mcc_optimize(problem(), _criteria.type, _criteria.maxCount, _criteria.epsilon, x.data(), &_iters,
                            &_change));
@@ -253,11 +254,16 @@ public:
     // src/multicalib.cpp:624, 629; src/doubleSide.cpp:472, 480) and, for pinhole cameras, every
     // projected corner inside the 1920 x 1080 image (IsvalidImagePoints, src/multicalib.cpp:704-715,
     // asserted at src/mymulticalib.cpp:568 and src/doubleSide.cpp:378).  A failed assert aborts.
+    // With verbose output (the constructor's `verbose`, or MCC_VERBOSE=1) the same host loop prints
+    // the reference's per-iteration lines (src/multicalib.cpp:492, 499-500, 506): alpha_smooth2, the
+    // parameters and the step as OpenCV prints a 1 x P CV_32F Mat, iter / change.
     double optimizeExtrinsicsChecked() {
-        for (const edge& e : _edgeList) {
-            const float t[3] = {e.transform[3], e.transform[7], e.transform[11]};
-            if (!valid_pose(t)) strict_abort("isValidPose(Tvectran)", "src/mymulticalib.cpp:706");
-        }
+        if (strictReference)
+            for (const edge& e : _edgeList) {
+                const float t[3] = {e.transform[3], e.transform[7], e.transform[11]};
+                if (!valid_pose(t)) strict_abort("isValidPose(Tvectran)", "src/mymulticalib.cpp:706");
+            }
+        const bool print = verboseOn();
         std::vector<float> x = buildParaVector();
         double change = 1.0;
         int iter = 0;
@@ -266,18 +272,25 @@ public:
             if ((ty == 1 && iter >= _criteria.maxCount) || (ty == 2 && change <= _criteria.epsilon) ||
                 (ty == 3 && (change <= _criteria.epsilon || iter >= _criteria.maxCount)))
                 break;
-            checkIterate(x);
+            if (strictReference) checkIterate(x);
             std::vector<double> jinv, jte, delta;
             computeJacobianExtrinsic(x, jinv, jte, delta);
             const double alpha = std::pow(0.95, (double)iter + 1.0);
+            std::vector<float> G(x.size());
+            for (size_t i = 0; i < x.size(); ++i) G[i] = (float)(alpha * delta[i]);
+            if (print) {
+                std::printf("alpha_smooth2:%s \n", cout_str(alpha).c_str());
+                print_row("extrinParam:", x);
+                print_row("Gt:", G);
+            }
             double g2 = 0.0, x2 = 0.0;
             for (size_t i = 0; i < x.size(); ++i) {
-                const float G = (float)(alpha * delta[i]);
-                x[i] = x[i] + G;
-                g2 += (double)G * G;
+                x[i] = x[i] + G[i];
+                g2 += (double)G[i] * G[i];
             }
             for (float v : x) x2 += (double)v * v;
             change = std::sqrt(g2) / std::sqrt(x2);
+            if (print) std::printf("iter:%d" "change:%s\n", iter, cout_str(change).c_str());
         }
         _iters = iter;
         _change = change;
@@ -346,12 +359,68 @@ public:
 
     // computeProjectError (multicalib.hpp:188): fills every edge's reprojecterror (per-edge mean
     // L2 error, float) and returns the reference's mean
+    // With verbose output it also prints what the reference prints (src/mymulticalib.cpp:919-937,
+    // src/multicalib.cpp:986-1004): every edge's reprojecterror, largest first, with its corner file
+    // (printedgelist, :889-894), totalError, totalNPoints, meanReProjError and the float32 standard
+    // deviation of the per-corner errors about the mean.
     virtual double computeProjectError(std::vector<float>& parameters) {
         std::vector<float> err(_edgeList.size());
         double mean = 0.0;
-        check(mcc_project_error(problem(), parameters.data(), err.data(), &mean));
+        if (!verboseOn()) {
+            check(mcc_project_error(problem(), parameters.data(), err.data(), &mean));
+            for (size_t e = 0; e < _edgeList.size(); ++e) _edgeList[e].reprojecterror = err[e];
+            return mean;
+        }
+        long long corners = 0, npts = 0;
+        check(mcc_problem_stats(problem(), &corners, nullptr, nullptr, nullptr));
+        std::vector<float> cerr((size_t)corners);
+        float total = 0.f;
+        check(mcc_project_error_detail(problem(), parameters.data(), err.data(), cerr.data(), &total, &npts, &mean));
         for (size_t e = 0; e < _edgeList.size(); ++e) _edgeList[e].reprojecterror = err[e];
+        std::vector<size_t> order(_edgeList.size());
+        for (size_t e = 0; e < order.size(); ++e) order[e] = e;
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return err[a] > err[b]; });
+        for (size_t e : order) {
+            const edge& eg = _edgeList[e];
+            const bool named = eg.cameraVertex < (int)filesEachCameraFull.size() &&
+                               eg.photoIndex < (int)filesEachCameraFull[eg.cameraVertex].size();
+            const std::string f = named ? filesEachCameraFull[eg.cameraVertex][eg.photoIndex]
+                                        : "camera " + std::to_string(eg.cameraVertex) + " view " + std::to_string(eg.photoIndex);
+            std::printf("%s:%s\n", cout_str(eg.reprojecterror).c_str(), f.c_str());
+        }
+        std::printf("totalError:%s\n", cout_str(total).c_str());
+        std::printf("totalNPoints:%lld\n", npts);
+        std::printf("meanReProjError:%s\n", cout_str(mean).c_str());
+        float var = 0;
+        for (float v : cerr) var += (v - mean) * (v - mean);
+        var /= cerr.size();
+        const float sd = std::sqrt(var);
+        std::printf("standard deviation of ReProjError:%s\n", cout_str(sd).c_str());
+        std::fflush(stdout);
         return mean;
+    }
+    // verbose output: the constructor's `verbose` or MCC_VERBOSE=1
+    bool verboseOn() const {
+        const char* v = std::getenv("MCC_VERBOSE");
+        return _verbose || (v && std::atoi(v) != 0);
+    }
+    // std::cout's default formatting of a number (precision 6, %g)
+    static std::string cout_str(double v) {
+        char b[48];
+        std::snprintf(b, sizeof b, "%g", v);
+        return b;
+    }
+    // OpenCV's default format of a 1 x P CV_32F Mat: "[v0, v1, ...]" with %.8g
+    static void print_row(const char* name, const std::vector<float>& v) {
+        std::string o = name;
+        o += "[";
+        char b[48];
+        for (size_t i = 0; i < v.size(); ++i) {
+            std::snprintf(b, sizeof b, i ? ", %.8g" : "%.8g", (double)v[i]);
+            o += b;
+        }
+        o += "]\n";
+        std::fputs(o.c_str(), stdout);
     }
 
     // buildParas (src/multicalib.cpp:422-440): [vertex 1 .. nVertex-1] x (rvec, tvec)

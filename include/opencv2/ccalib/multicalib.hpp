@@ -207,8 +207,15 @@ public:
             Mat G = alpha_smooth2 * deltx;
             if (G.depth() == CV_64F) G.convertTo(G, CV_32F);
             const Mat Gt = G.reshape(1, 1);
+            const bool print = this->verboseOn();   // src/multicalib.cpp:492, 499-500, 506
+            if (print) {
+                std::printf("alpha_smooth2:%s \n", this->cout_str(alpha_smooth2).c_str());
+                this->print_row("extrinParam:", detail::to_f32(extrinParam));
+                this->print_row("Gt:", detail::to_f32(Gt));
+            }
             extrinParam = extrinParam + Gt;
             change = norm(G) / norm(extrinParam);
+            if (print) std::printf("iter:%d" "change:%s\n", iter, this->cout_str(change).c_str());
         }
         this->_iters = iter;
         this->_change = change;

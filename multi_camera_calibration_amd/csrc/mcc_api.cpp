@@ -168,7 +168,7 @@ struct mcc_problem {
     std::vector<int> edge_n_dev;
 
     // device buffers
-    DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum;
+    DevBuf<float> obj_x, obj_y, obj_z, img_u, img_v, x, xerr, K, D, xi, cam_rt, cam_pose, resid, edge_sum, corner_err;
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
@@ -955,7 +955,7 @@ void mcc_destroy(mcc_problem* p) {
     if (p->inbox) (void)hipFree(p->inbox);
     p->obj_x.release(); p->obj_y.release(); p->obj_z.release(); p->img_u.release(); p->img_v.release();
     p->x.release(); p->xerr.release(); p->K.release(); p->D.release(); p->xi.release(); p->cam_rt.release();
-    p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->stamps.release();
+    p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->corner_err.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
     p->erec.release(); p->echain.release(); p->eh.release();
@@ -1073,17 +1073,25 @@ int mcc_check(mcc_problem* p) {
     return rc;
 }
 
-int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* mean) {
+int mcc_project_error_detail(mcc_problem* p, const float* x, float* edge_err, float* corner_err, float* total_error,
+                             long long* total_points, double* mean) {
     if (!p || !x) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->xerr.p, x, sizeof(float) * p->P, hipMemcpyHostToDevice));
+    if (corner_err && !p->corner_err.p) HIPCHK(p->corner_err.alloc(std::max<long long>(p->corners, 1)));
     mcc::ErrArgs a{p->edge_info.p, p->edge_photo.p, p->obj_x.p, p->obj_y.p, p->obj_z.p, p->img_u.p, p->img_v.p,
-                   p->xerr.p, p->K.p, p->D.p, p->xi.p, p->cam_pose.p, p->edge_sum.p, p->nd, p->m};
+                   p->xerr.p, p->K.p, p->D.p, p->xi.p, p->cam_pose.p, p->edge_sum.p,
+                   corner_err ? p->corner_err.p : nullptr, p->nd, p->m};
     if (p->E) HIPCHK(mcc_launch_project_error(a, p->model, p->E, p->rational, p->prism, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
     std::vector<float> sums(p->E);
     if (p->E) HIPCHK(hipMemcpy(sums.data(), p->edge_sum.p, sizeof(float) * p->E, hipMemcpyDeviceToHost));
+    if (corner_err && p->corners) {
+        std::vector<float> ce(p->corners);
+        HIPCHK(hipMemcpy(ce.data(), p->corner_err.p, sizeof(float) * p->corners, hipMemcpyDeviceToHost));
+        for (long long c = 0; c < p->corners; ++c) corner_err[p->dev2ref_corner[c]] = ce[c];
+    }
     std::vector<float> by_ref(p->E);
     std::vector<int> n_ref(p->E);
     for (int de = 0; de < p->E; ++de) {
@@ -1098,8 +1106,14 @@ int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* m
         total += by_ref[e];
         npts += p->model == MCC_MODEL_OMNI ? n_ref[e] : 2LL * n_ref[e];   // error.total() (H2)
     }
+    if (total_error) *total_error = total;
+    if (total_points) *total_points = npts;
     if (mean) *mean = npts ? (double)total / (double)npts : 0.0;
     return MCC_OK;
+}
+
+int mcc_project_error(mcc_problem* p, const float* x, float* edge_err, double* mean) {
+    return mcc_project_error_detail(p, x, edge_err, nullptr, nullptr, nullptr, mean);
 }
 
 int mcc_debug_solve(int device, int m, const double* packed, double* x, int reps, double* us_per_solve,

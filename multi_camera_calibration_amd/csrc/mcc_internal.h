@@ -275,6 +275,7 @@ struct ErrArgs {
     const float* K; const float* D; const float* xi;
     const float* cam_pose;   // DOUBLESIDE [16C]
     float* edge_sum;         // [E] device order
+    float* corner_err;       // optional [corners] device order: each corner's float32 L2 error
     int nd, m;
 };
 

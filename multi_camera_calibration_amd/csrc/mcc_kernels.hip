@@ -3587,6 +3587,7 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
         float s2 = ex * ex;
         s2 = s2 + ey * ey;
         ferr[i] = sqrtf(s2);
+        if (a.corner_err) a.corner_err[c] = ferr[i];
     }
     __syncthreads();
     if (lane == 0) {

@@ -186,3 +186,71 @@ def test_seam_subclass_with_reference_body(seam_exe, tmp_path, path):
     r = subprocess.run([seam_exe, "refstyle", str(tmp_path / "in.bin")], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "refstyle ok" in r.stdout
+
+
+def _blocks(stdout):
+    """Split the verbose output into optimize runs: [(iters, rows, tail)]; iters are (alpha, x, G,
+    k, change), tail the computeProjectError block that ends the run."""
+    lines = stdout.splitlines()
+    runs, cur, tail = [], [], []
+    i = 0
+    while i < len(lines):
+        ln = lines[i]
+        if ln.startswith("alpha_smooth2:"):
+            a = float(ln.split(":")[1])
+            x = np.array([float(v) for v in lines[i + 1][len("extrinParam:["):-1].split(",")])
+            g = np.array([float(v) for v in lines[i + 2][len("Gt:["):-1].split(",")])
+            k, ch = lines[i + 3][len("iter:"):].split("change:")
+            cur.append((a, x, g, int(k), float(ch)))
+            i += 4
+            continue
+        tail.append(ln)
+        if ln.startswith("standard deviation of ReProjError:"):
+            runs.append((cur, tail))
+            cur, tail = [], []
+        i += 1
+    return runs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", [f for f in FIXTURES if "config1" in f or "config4" in f or "config5_v8" in f],
+                         ids=lambda f: os.path.splitext(os.path.basename(f))[0])
+def test_cpp_host_verbose_lines(exe, tmp_path, path):
+    """MCC_VERBOSE=1 (or the constructor's verbose): the reference's printed lines, for diffing
+    against its logs -- per Gauss-Newton iteration alpha_smooth2, extrinParam, Gt and iter / change
+    (src/multicalib.cpp:492, 499-500, 506), and after the loop every edge's reprojecterror largest
+    first, totalError, totalNPoints, meanReProjError and the standard deviation
+    (src/mymulticalib.cpp:919-937).  The numbers are the run's own: alpha = 0.95^(k+1), x_{k+1} =
+    x_k + G_k, change = |G| / |x_{k+1}|, the printed mean is the returned error."""
+    gd = dict(np.load(path))
+    p = _write_blob(str(tmp_path / "in.bin"), gd)
+    env = dict(os.environ, MCC_VERBOSE="1")
+    r = subprocess.run([exe, "run", str(tmp_path / "in.bin"), str(tmp_path / "out.txt")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    o = _read_out(str(tmp_path / "out.txt"))
+    runs = _blocks(r.stdout)
+    assert len(runs) == 3   # computeProjectError at x0, then two optimizeExtrinsics
+    iters, tail = runs[1]
+    assert len(iters) == int(o["opt_iters"][0]) and [k for *_, k, _ in iters] == list(range(len(iters)))
+    for k, (a, x, g, _, ch) in enumerate(iters):
+        assert abs(a - 0.95 ** (k + 1)) <= 1e-6 * a
+        assert x.size == g.size == p.x0.size
+        x1 = (x.astype(np.float32) + g.astype(np.float32)).astype(np.float64)
+        assert abs(ch - np.linalg.norm(g) / np.linalg.norm(x1)) <= 1e-4 * ch + 1e-12
+        if k + 1 < len(iters):
+            assert np.abs(iters[k + 1][1] - x1).max() <= 1e-6 * np.abs(x1).max()
+    np.testing.assert_allclose(iters[0][1], o["x_built"], rtol=1e-7, atol=1e-7)
+    edges = [ln for ln in tail if ":" in ln and not ln.split(":")[0].isalpha() and not ln.startswith(("total", "mean", "standard"))]
+    errs = [float(ln.split(":")[0]) for ln in edges]
+    assert len(errs) == p.n_edges and errs == sorted(errs, reverse=True)
+    kv = {ln.split(":")[0]: float(ln.split(":")[1]) for ln in tail if ln.startswith(("total", "mean", "standard"))}
+    npts = int(np.asarray(p.edge_n).sum()) * (1 if p.model == rig.OMNI else 2)
+    assert int(kv["totalNPoints"]) == npts
+    assert abs(kv["meanReProjError"] - o["opt_error"][0]) <= 1e-5 * o["opt_error"][0]
+    assert abs(kv["totalError"] / npts - o["opt_error"][0]) <= 1e-4 * o["opt_error"][0]
+    assert 0.0 < kv["standard deviation of ReProjError"] < 10.0
+    # quiet by default
+    r2 = subprocess.run([exe, "run", str(tmp_path / "in.bin"), str(tmp_path / "out2.txt")], capture_output=True,
+                        text=True, timeout=300)
+    assert "alpha_smooth2" not in r2.stdout and "meanReProjError" not in r2.stdout
