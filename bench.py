@@ -54,6 +54,7 @@ from multi_camera_calibration_amd import api, rig  # noqa: E402
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_PEAK_TFS = 78.6    # MI355X FP64 vector peak, AMD spec
 METRIC = "corner residual+Jacobian evals/sec + ms/LM-iter; RMS reproj-err vs ref"
+DIST_WINDOWS, DIST_STEPS = 30, 20   # the per-step distribution: 30 windows of 20 steps
 
 
 def _launch_key() -> str:
@@ -157,13 +158,22 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
     ba.timing_begin()
     ba.step(window)
     lin_ms, step_ms_ev, nlaunch = ba.timing_end()
+    mode = ba.timing_mode()
     xchg_ms, n_xchg = ba.timing_exchange()
     ba.check()   # a failed step (peer timeout, not PD) stops the later ones: never report that as speed
     lin_ms = ba.allreduce_max(lin_ms)
     step_ms_ev = ba.allreduce_max(step_ms_ev)
     xchg_ms = ba.allreduce_max(xchg_ms)
+    # per-step distribution (SURVEY.md 8(d) / BASELINE.md section 3: median, p10, p90): DIST_WINDOWS
+    # back-to-back windows of DIST_STEPS graph-launched steps, each timed by HIP events on the step stream
+    wins, graph = ba.timing_windows(DIST_WINDOWS, DIST_STEPS)
+    ba.check()
+    per = wins / DIST_STEPS
+    dist = {q: ba.allreduce_max(float(np.percentile(per, v))) for q, v in (("p10", 10), ("median", 50), ("p90", 90))}
+    dist.update(unit="ms per step", windows=DIST_WINDOWS, steps_per_window=DIST_STEPS,
+                launch="graph" if graph else "eager", timer="HIP events between back-to-back windows (max over ranks)")
     return dict(dt=dt, lin_ms=lin_ms, step_ms_ev=step_ms_ev, nlaunch=nlaunch, xchg_ms=xchg_ms, n_xchg=n_xchg,
-                ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)})
+                ramp={"steps": n_ramp + 24, "seconds": round(ramp_wall, 3)}, timing_mode=mode, dist=dist)
 
 
 def lin_kernels(ba) -> str:
@@ -172,9 +182,12 @@ def lin_kernels(ba) -> str:
     return ba.step_kernels()
 
 
-def roofline(st, lin_ms, tr=None, kernel="k_linearize"):
+def roofline(st, lin_ms, tr=None, kernel="k_linearize", mode="graph"):
     achieved = st["alg_bytes"] / (lin_ms * 1e-3) / 1e9
     return {
+        "kernel_timing": ("HIP events around the kernel inside graph-launched steps (the window's steps "
+                          "captured with their event records as one graph)" if mode == "graph" else
+                          "HIP events around eagerly launched kernels"),
         "bound": "hbm",
         "kernel": kernel,
         "achieved": achieved,
@@ -219,7 +232,9 @@ def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
            "model": {rig.PINHOLE: "pinhole", rig.OMNI: "omnidir", rig.DOUBLESIDE: "doubleside"}[p.model],
            "steps": steps, "ms_per_step": ms, "corner_evals_per_s": p.n_corners / (ms * 1e-3),
            "step_ms_events": m["step_ms_ev"], "launches_timed": m["nlaunch"],
-           "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=kern),
+           "roofline": roofline(st, m["lin_ms"], load_profile("traffic", name, p.n_photos), kernel=kern,
+                                mode=m["timing_mode"]),
+           "step_distribution": m["dist"],
            "rig_generation_s": round(gen_s, 2)}
     if solve["warm"] or solve["direct"]:
         # m > 30: solves by refinement with the previous step's inverse (k_sinv, side stream) over
@@ -264,6 +279,31 @@ def strong_line(name: str, rank: int, world: int, local_rank: int, same_device: 
     return out
 
 
+def shard_line(name: str, world: int, steps: int = 200, device: int = 0):
+    """The compute side of the strong-scaling curve, on this one GPU: rank 0's photo shard of a
+    BASELINE multi-GPU rig split `world` ways (mcc_partition_photos), timed as a standalone problem --
+    its linearisation, reduction, the replicated camera solve and the update; the exchange is what it
+    leaves out.  full / shard is the speedup bound of that split before exchange costs."""
+    full = rig.make_config(name)
+    owner = api.partition_photos(full, world)
+    prob = rig.subset_photos(full, np.nonzero(owner == 0)[0])
+    ba = api.BundleAdjuster(prob, device=device)
+    try:
+        ba.set_params(prob.x0)
+        m = measure(ba, steps, 10, 0.15, max(100, steps))
+        kern = lin_kernels(ba)
+        solve = ba.solve_stats()
+    finally:
+        ba.close()
+    ms = m["dt"] / steps * 1e3
+    out = {"split": world, "views": prob.n_photos, "edges": prob.n_edges, "corners_per_step": prob.n_corners,
+           "ms_per_step": ms, "step_distribution": m["dist"], "kernel": kern, "kernel_ms_per_launch": m["lin_ms"],
+           "exchange": "excluded (single process: no peers)"}
+    if solve["warm"] or solve["direct"]:
+        out["warm_solve"] = solve
+    return out
+
+
 def cpu_baseline(prob, target_s: float):
     """The oracle (the C restatement of the reference algorithm, block-sparse Schur variant,
     OpenMP over the host cores) timed on a bounded sample of the same workload."""
@@ -302,8 +342,19 @@ def cpu_baseline_ref_faithful():
                 ms_per_step=dt / it * 1e3, iterations=it, meanReProjError=mean,
                 sample=f"config1 (2 cameras, 20 views, 9x6 board): the whole optimizeExtrinsics, {it} steps of dense "
                        f"J ({rows} x {p.n_params}) + J^T J + Jacobi-CG x2, single thread, {dt:.3f} s wall",
-                config2="skipped: its dense J is 345k x 3018 doubles (8.3 GB) and J^T J alone is ~1.6e12 "
-                        "multiply-adds per step (tens of minutes on one core), beyond a bench run")
+                config2=_ref_faithful_config2())
+
+
+def _ref_faithful_config2():
+    """config2's one-iteration ref-faithful timing: 8.3 GB of dense J and ~1.6e12 multiply-adds of
+    J^T J per step take tens of minutes on one core, so it is run offline once
+    (tools/ref_faithful_config2.py) and the committed result is cited here."""
+    f = os.path.join(ROOT, "profiles", "ref_faithful_config2.json")
+    if os.path.exists(f):
+        d = json.load(open(f))
+        d["source"] = "profiles/ref_faithful_config2.json (tools/ref_faithful_config2.py, offline, not this run)"
+        return d
+    return "not run: tools/ref_faithful_config2.py has not produced profiles/ref_faithful_config2.json"
 
 
 def main():
@@ -357,7 +408,7 @@ def main():
         return
     tr = load_profile("traffic", args.config, views_per_rank) if world == 1 else None
     model = MODEL_NAMES[rig.CONFIGS[args.config]["model"]]
-    rl = roofline(st, m["lin_ms"], tr, kernel=kern)
+    rl = roofline(st, m["lin_ms"], tr, kernel=kern, mode=m["timing_mode"])
     rl["kernel_launches_timed"] = m["nlaunch"]
     rl["step_ms_events"] = m["step_ms_ev"]
     out = {
@@ -385,6 +436,7 @@ def main():
             "state_dtype": "f32", "jacobian_dtype": "f64",
         },
         "clock_ramp": m["ramp"],
+        "step_distribution": m["dist"],
         "exchange_ms": m["xchg_ms"] if world > 1 else None,
         "roofline": rl,
     }
@@ -413,6 +465,15 @@ def main():
     if world == 1 and not args.no_extra:
         out["configs"] = {name: config_line(name, device=local_rank)
                           for name in ("config2", "config3", "config4", "config5") if name != args.config}
+        # BASELINE's multi-GPU rigs: rank 0's shard at the rank counts they are quoted on, timed here
+        out["shard"] = {}
+        for name, w in (("config3", 8), ("config5", 4)):
+            sl = shard_line(name, w, device=local_rank)
+            full_ms = out["configs"][name]["ms_per_step"] if name in out["configs"] else None
+            if full_ms:
+                sl["full_ms_per_step"] = full_ms
+                sl["compute_speedup_bound"] = full_ms / sl["ms_per_step"]
+            out["shard"][f"{name}_x{w}"] = sl
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(prob, args.cpu_seconds)
         out["cpu_baseline_ref_faithful"] = cpu_baseline_ref_faithful()

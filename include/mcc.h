@@ -185,9 +185,19 @@ int mcc_debug_solve(int device, int m, const double *packed, double *x, int reps
  * mcc_timing_begin/mcc_timing_end window (HIP events on the problem's stream), and launches.
  * Fused single-GPU problems (m <= 30 and at most two photos per CU: one kernel per step) time
  * the whole window of graph-launched steps with two events; split-step problems record an event
- * pair around the k_prep + k_edge + k_photo launches of every step (eager). */
+ * pair around the linearisation kernels (k_group, or k_prep + k_edge + k_photo) of every step and
+ * one around the whole step, the window's steps captured with those event records as one graph
+ * (mcc_timing_mode says whether the capture held: 1, or the steps ran eagerly: 0). */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
+/* 1 when the last timing window's steps were graph-launched (the window's steps are captured with
+ * their event records as one graph), 0 when they fell back to eager launches */
+int mcc_timing_mode(const mcc_problem *p);
+/* per-step time distribution: n_windows windows of `steps` free-running steps each, enqueued back to
+ * back (graph-launched as mcc_step launches them) with a HIP event between windows; ms_per_window[i]
+ * is window i's device time (a leading window, which would include the idle gap before the first
+ * launch, is run and dropped).  *graph_launched = 1 when the steps ran as graphs. */
+int mcc_timing_windows(mcc_problem *p, int n_windows, int steps, double *ms_per_window, int *graph_launched);
 /* average time (ms) of the step's data-path exchange over the same window, and the exchanges:
  * RCCL all-reduces by HIP event pairs around each ncclAllReduce, the peer transport by the
  * device's own s_memrealtime ticks from the first send to the rank-ordered sums (in-kernel, so

@@ -83,10 +83,31 @@ inline void rodrigues_v2m(const float rv[3], float R[9]) {
     for (int k = 0; k < 9; ++k) R[k] = (float)(c * ((k % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[k] + s * rx_[k]);
 }
 
-// cvRodrigues2, matrix -> vector (trace / skew formula with the theta ~ 0 and ~ pi branches)
+// the orthonormal polar factor U V^T of a near-rotation (cvRodrigues2 takes it by SVD before the
+// matrix -> vector formula), by the Newton iteration R <- (R + R^-T) / 2
+inline void polar_orthonormalise(double R[9]) {
+    for (int it = 0; it < 40; ++it) {
+        const double cof[9] = {R[4] * R[8] - R[5] * R[7], -(R[3] * R[8] - R[5] * R[6]), R[3] * R[7] - R[4] * R[6],
+                               -(R[1] * R[8] - R[2] * R[7]), R[0] * R[8] - R[2] * R[6], -(R[0] * R[7] - R[1] * R[6]),
+                               R[1] * R[5] - R[2] * R[4], -(R[0] * R[5] - R[2] * R[3]), R[0] * R[4] - R[1] * R[3]};
+        const double d = R[0] * cof[0] + R[1] * cof[1] + R[2] * cof[2];
+        if (!(std::fabs(d) > 1e-300)) return;
+        double delta = 0;
+        for (int k = 0; k < 9; ++k) {
+            const double v = 0.5 * (R[k] + cof[k] / d);
+            delta = std::max(delta, std::fabs(v - R[k]));
+            R[k] = v;
+        }
+        if (delta < 1e-15) return;
+    }
+}
+
+// cvRodrigues2, matrix -> vector (polar factor, then the trace / skew formula with the theta ~ 0
+// and ~ pi branches), evaluated in double for a float matrix
 inline void rodrigues_m2v(const float Rf[9], float rv[3]) {
     double R[9];
     for (int k = 0; k < 9; ++k) R[k] = Rf[k];
+    polar_orthonormalise(R);
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;

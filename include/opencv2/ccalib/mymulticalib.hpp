@@ -53,6 +53,7 @@ protected:
         double R[9], r[3];
         for (int i = 0; i < 3; ++i)
             for (int j = 0; j < 3; ++j) R[3 * i + j] = this->doubleSideTransform[4 * i + j];
+        mcc::multicalib::polar_orthonormalise(R);   // cv::Rodrigues' SVD step
         mcc::pnp::rodriguesInv(R, r);
         Mat m(3, 1, CV_64F);
         for (int k = 0; k < 3; ++k) m.at<double>(k, 0) = r[k];

@@ -111,6 +111,10 @@ def lib():
         L.mcc_timing_begin.argtypes = [ctypes.c_void_p]
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_timing_exchange.argtypes = [ctypes.c_void_p, _f64p, _i32p]
+        L.mcc_timing_windows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f64p, _i32p]
+        L.mcc_timing_mode.argtypes = [ctypes.c_void_p]
+        L.mcc_project_error_detail.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p, _f32p,
+                                               ctypes.POINTER(ctypes.c_longlong), _f64p]
         L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
         L.mcc_solve_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_longlong)]
         L.mcc_problem_path.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -323,6 +327,31 @@ class BundleAdjuster:
         n = ctypes.c_int(0)
         _check(lib().mcc_timing_end(self.h, ctypes.byref(lin), ctypes.byref(st), ctypes.byref(n)), "mcc_timing_end")
         return lin.value, st.value, n.value
+
+    def timing_windows(self, n_windows, steps):
+        """Device time (ms) of each of n_windows back-to-back windows of `steps` free-running steps
+        (mcc_timing_windows), and whether they ran graph-launched."""
+        out = np.zeros(n_windows)
+        g = ctypes.c_int(0)
+        _check(lib().mcc_timing_windows(self.h, n_windows, steps, _ptr(out, _f64p), ctypes.byref(g)), "mcc_timing_windows")
+        return out, bool(g.value)
+
+    def timing_mode(self):
+        """'graph' when the last timing window's steps ran graph-launched, else 'eager'."""
+        return "graph" if lib().mcc_timing_mode(self.h) == 1 else "eager"
+
+    def project_error_detail(self, x):
+        """(edge errors, per-corner L2 errors in reference order, totalError, totalNPoints, mean)."""
+        x = np.ascontiguousarray(x, np.float32)
+        err = np.zeros(self.prob.n_edges, np.float32)
+        cerr = np.zeros(self.prob.n_corners, np.float32)
+        tot = ctypes.c_float(0)
+        npts = ctypes.c_longlong(0)
+        mean = ctypes.c_double(0)
+        _check(lib().mcc_project_error_detail(self.h, _ptr(x, _f32p), _ptr(err, _f32p), _ptr(cerr, _f32p),
+                                              ctypes.byref(tot), ctypes.byref(npts), ctypes.byref(mean)),
+               "mcc_project_error_detail")
+        return err, cerr, tot.value, npts.value, mean.value
 
     def timing_exchange(self):
         """(ms per data-path exchange, exchanges) over the last timing window (mcc_timing_exchange)."""

@@ -232,6 +232,9 @@ struct mcc_problem {
 
     // timing window
     bool timing = false;
+    bool timing_eager = false;               // the window's capture failed once: eager launches
+    std::vector<hipGraphExec_t> timed_execs;   // the window's one-off graphs (destroyed at mcc_timing_end)
+    std::vector<hipEvent_t> ev_marks;        // mcc_timing_windows
     std::vector<hipEvent_t> ev_lin, ev_step;
     int ev_used = 0;
     // fused single-kernel step: the window is timed by two events around graph-launched steps
@@ -423,25 +426,59 @@ int build_graph(mcc_problem* p, int k) {
     HIPCHK(hipGraphDestroy(graph));
     return MCC_OK;
 }
+// the timing window's steps (mcc_timing_begin): captured with their event records as ONE graph and
+// launched like the product's graphs, so the kernel times it reports come from graph-launched steps
+// (the eager form, kept as a fallback, adds a host launch per kernel); the graph is dropped at
+// mcc_timing_end
+int capture_timed(mcc_problem* p, int n, hipGraphExec_t* out) {
+    *out = nullptr;
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+    const int used0 = p->ev_used, x0 = p->ev_x_used;
+    int rc = MCC_OK;
+    for (int s = 0; s < n && rc == MCC_OK; ++s) rc = enqueue_step(p, 1, nullptr);
+    hipError_t ee = hipStreamEndCapture(p->stream, &graph);
+    hipError_t ei = ee == hipSuccess && rc == MCC_OK ? hipGraphInstantiate(out, graph, nullptr, nullptr, 0) : ee;
+    if (ee == hipSuccess) (void)hipGraphDestroy(graph);
+    if (rc != MCC_OK || ee != hipSuccess || ei != hipSuccess) {   // eager fallback: no step of the capture ran
+        (void)hipGetLastError();
+        *out = nullptr;
+        p->ev_used = used0;
+        p->ev_x_used = x0;
+        p->timing_eager = true;
+    }
+    return MCC_OK;
+}
+
 int launch_update_steps(mcc_problem* p, int n) {
     if (p->timing_window) p->win_steps += n;
-    const bool eager = p->timing || !p->use_graph;
-    // every graph of this batch exists before the batch's helper starts: instantiating a 64-step
-    // graph takes milliseconds, which the helper would otherwise spend polling for the first system
-    if (!eager)
+    bool eager = !p->use_graph || (p->timing && p->timing_eager);
+    hipGraphExec_t timed = nullptr;
+    if (!eager && p->timing) {
+        int rc = capture_timed(p, n, &timed);
+        if (rc) return rc;
+        eager = timed == nullptr;
+    } else if (!eager) {
+        // every graph of this batch exists before the batch's helper starts: instantiating a 64-step
+        // graph takes milliseconds, which the helper would otherwise spend polling for the first system
         for (int k = p->graph_sizes - 1, r = n; k >= 0; --k)
             if (r >= (1 << k)) {
                 int rc = build_graph(p, k);
                 if (rc) return rc;
                 r -= (r >> k) << k;
             }
+    }
     if (p->warm && n > 0) {
         // the batch's helper: after the previous one (side-stream order), with the stop flag cleared
         HIPCHK(hipMemsetAsync(p->wsync + 2, 0, sizeof(unsigned), p->side));
         HIPCHK(mcc_launch_sinv_helper(warm_ctx(p), p->m, n, p->side));
     }
     int rc = MCC_OK;
-    if (eager) {
+    if (timed) {
+        p->timed_execs.push_back(timed);
+        hipError_t e = hipGraphLaunch(timed, p->stream);
+        if (e != hipSuccess) rc = fail(MCC_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+    } else if (eager) {
         for (int i = 0; i < n && rc == MCC_OK; ++i) rc = enqueue_step(p, 1, nullptr);
     } else {
         for (int k = p->graph_sizes - 1; k >= 0 && rc == MCC_OK; --k)
@@ -947,6 +984,8 @@ void mcc_destroy(mcc_problem* p) {
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
     for (auto e : p->ev_x) (void)hipEventDestroy(e);
+    for (auto e : p->ev_marks) (void)hipEventDestroy(e);
+    for (auto g : p->timed_execs) (void)hipGraphExecDestroy(g);
     for (auto e : p->ev_win) if (e) (void)hipEventDestroy(e);
     if (p->comm) (void)ncclCommDestroy(p->comm);
     for (void* m : p->peer_mapped) (void)hipIpcCloseMemHandle(m);
@@ -1263,6 +1302,8 @@ int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launche
         return MCC_OK;
     }
     HIPCHK(hipStreamSynchronize(p->stream));
+    for (auto g : p->timed_execs) (void)hipGraphExecDestroy(g);
+    p->timed_execs.clear();
     double lin = 0, st = 0;
     const int n = p->ev_used / 2;
     for (int i = 0; i < n; ++i) {
@@ -1277,6 +1318,44 @@ int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launche
     if (step_ms) *step_ms = n ? st / n : 0.0;
     if (launches) *launches = n;
     return MCC_OK;
+}
+
+int mcc_timing_windows(mcc_problem* p, int n_windows, int steps, double* ms_per_window, int* graph_launched) {
+    if (!p || n_windows < 1 || steps < 1 || !ms_per_window) return fail(MCC_EINVAL, "bad timing-window arguments");
+    HIPCHK(hipSetDevice(p->device));
+    if (p->timing || p->timing_window) return fail(MCC_EINVAL, "mcc_timing_windows inside a timing window");
+    if (!p->stepping) {
+        int rc = set_state(p, 0, 0, 0, 0.0);
+        if (rc) return rc;
+        p->stepping = true;
+    }
+    if ((int)p->ev_marks.size() < n_windows + 2) {
+        const size_t old = p->ev_marks.size();
+        p->ev_marks.resize(n_windows + 2);
+        for (size_t i = old; i < p->ev_marks.size(); ++i) HIPCHK(hipEventCreate(&p->ev_marks[i]));
+    }
+    // n_windows + 1 windows back to back, each bracketed by an event on the step stream, enqueued
+    // before any wait: the GPU runs them without a gap, and the first one (which would include the
+    // idle time before the first graph arrives) is dropped
+    for (int w = 0; w <= n_windows; ++w) {
+        HIPCHK(hipEventRecord(p->ev_marks[w], p->stream));
+        int rc = launch_update_steps(p, steps);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventRecord(p->ev_marks[n_windows + 1], p->stream));
+    HIPCHK(hipEventSynchronize(p->ev_marks[n_windows + 1]));
+    for (int w = 1; w <= n_windows; ++w) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, p->ev_marks[w], p->ev_marks[w + 1]));
+        ms_per_window[w - 1] = ms;
+    }
+    if (graph_launched) *graph_launched = p->use_graph ? 1 : 0;
+    return MCC_OK;
+}
+
+int mcc_timing_mode(const mcc_problem* p) {
+    if (!p) return -1;
+    return p->timing_eager || !p->use_graph ? 0 : 1;
 }
 
 int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges) {

@@ -234,7 +234,7 @@ def test_cpp_host_verbose_lines(exe, tmp_path, path):
     iters, tail = runs[1]
     assert len(iters) == int(o["opt_iters"][0]) and [k for *_, k, _ in iters] == list(range(len(iters)))
     for k, (a, x, g, _, ch) in enumerate(iters):
-        assert abs(a - 0.95 ** (k + 1)) <= 1e-6 * a
+        assert abs(a - 0.95 ** (k + 1)) <= 5e-6 * a   # cout's 6 significant digits
         assert x.size == g.size == p.x0.size
         x1 = (x.astype(np.float32) + g.astype(np.float32)).astype(np.float64)
         assert abs(ch - np.linalg.norm(g) / np.linalg.norm(x1)) <= 1e-4 * ch + 1e-12

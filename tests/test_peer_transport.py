@@ -10,7 +10,8 @@ problem by the ORACLE (the single-GPU bars of tests/test_gpu_parity.py / test_fu
   * optimizeExtrinsics: iteration count, meanReProjError and the float32 parameters;
   * mcc_comm_allreduce_max over the transport.
 World 2 on every case, world 4 on config3_small (the N > 2 inbox and rank-order paths) and on
-config5_full (the 4-GPU rig BASELINE.json names).
+config5_full (the 4-GPU rig BASELINE.json names), world 8 on config3_full (the 8-GPU rig: eight
+625-view shards, the m = 90 push / receive across eight inboxes, eight warm-solve helpers).
 The fused path (config2, config5 DoubleSide) exchanges in k_linearize, the m <= 30 split step
 (config4_split: k_group -> k_schur, forced by MCC_FUSED=0) in k_schur's final arriver, the m > 30
 path (config3) in k_solve.  CPU: host-side argument checks.
@@ -79,7 +80,7 @@ def _eps(case, p):
 @pytest.mark.parametrize("case,world", [("config2_small", 2), ("config5_small", 2), ("config3_small", 2),
                                         ("config2_nocam", 2), ("config3_full", 2), ("config5_full", 2),
                                         ("config3_small", 4), ("config5_full", 4), ("config4_split", 2),
-                                        ("config4_split", 4)])
+                                        ("config4_split", 4), ("config3_full", 8)])
 def test_peer_ranks_one_device(case, world, tmp_path):
     """The sharded step against the ORACLE's optimizeExtrinsics on the whole problem
     (src/multicalib.cpp:462-514), at the single-GPU bars of tests/test_gpu_parity.py and
