@@ -186,13 +186,11 @@ int mcc_debug_solve(int device, int m, const double *packed, double *x, int reps
  * Fused single-GPU problems (m <= 30 and at most two photos per CU: one kernel per step) time
  * the whole window of graph-launched steps with two events; split-step problems record an event
  * pair around the linearisation kernels (k_group, or k_prep + k_edge + k_photo) of every step and
- * one around the whole step, the window's steps captured with those event records as one graph
- * (mcc_timing_mode says whether the capture held: 1, or the steps ran eagerly: 0). */
+ * one around the whole step, launched eagerly behind a ~5 ms device-side delay kernel, so that the
+ * whole window is queued before the GPU reaches it and runs back to back (no host launch latency
+ * between the kernels inside the event pairs). */
 int mcc_timing_begin(mcc_problem *p);
 int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, int *launches);
-/* 1 when the last timing window's steps were graph-launched (the window's steps are captured with
- * their event records as one graph), 0 when they fell back to eager launches */
-int mcc_timing_mode(const mcc_problem *p);
 /* per-step time distribution: n_windows windows of `steps` free-running steps each, enqueued back to
  * back (graph-launched as mcc_step launches them) with a HIP event between windows; ms_per_window[i]
  * is window i's device time (a leading window, which would include the idle gap before the first

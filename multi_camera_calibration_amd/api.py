@@ -112,7 +112,6 @@ def lib():
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_timing_exchange.argtypes = [ctypes.c_void_p, _f64p, _i32p]
         L.mcc_timing_windows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f64p, _i32p]
-        L.mcc_timing_mode.argtypes = [ctypes.c_void_p]
         L.mcc_project_error_detail.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p, _f32p,
                                                ctypes.POINTER(ctypes.c_longlong), _f64p]
         L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
@@ -335,10 +334,6 @@ class BundleAdjuster:
         g = ctypes.c_int(0)
         _check(lib().mcc_timing_windows(self.h, n_windows, steps, _ptr(out, _f64p), ctypes.byref(g)), "mcc_timing_windows")
         return out, bool(g.value)
-
-    def timing_mode(self):
-        """'graph' when the last timing window's steps ran graph-launched, else 'eager'."""
-        return "graph" if lib().mcc_timing_mode(self.h) == 1 else "eager"
 
     def project_error_detail(self, x):
         """(edge errors, per-corner L2 errors in reference order, totalError, totalNPoints, mean)."""

@@ -232,8 +232,6 @@ struct mcc_problem {
 
     // timing window
     bool timing = false;
-    bool timing_eager = false;               // the window's capture failed once: eager launches
-    std::vector<hipGraphExec_t> timed_execs;   // the window's one-off graphs (destroyed at mcc_timing_end)
     std::vector<hipEvent_t> ev_marks;        // mcc_timing_windows
     std::vector<hipEvent_t> ev_lin, ev_step;
     int ev_used = 0;
@@ -426,39 +424,14 @@ int build_graph(mcc_problem* p, int k) {
     HIPCHK(hipGraphDestroy(graph));
     return MCC_OK;
 }
-// the timing window's steps (mcc_timing_begin): captured with their event records as ONE graph and
-// launched like the product's graphs, so the kernel times it reports come from graph-launched steps
-// (the eager form, kept as a fallback, adds a host launch per kernel); the graph is dropped at
-// mcc_timing_end
-int capture_timed(mcc_problem* p, int n, hipGraphExec_t* out) {
-    *out = nullptr;
-    hipGraph_t graph;
-    HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
-    const int used0 = p->ev_used, x0 = p->ev_x_used;
-    int rc = MCC_OK;
-    for (int s = 0; s < n && rc == MCC_OK; ++s) rc = enqueue_step(p, 1, nullptr);
-    hipError_t ee = hipStreamEndCapture(p->stream, &graph);
-    hipError_t ei = ee == hipSuccess && rc == MCC_OK ? hipGraphInstantiate(out, graph, nullptr, nullptr, 0) : ee;
-    if (ee == hipSuccess) (void)hipGraphDestroy(graph);
-    if (rc != MCC_OK || ee != hipSuccess || ei != hipSuccess) {   // eager fallback: no step of the capture ran
-        (void)hipGetLastError();
-        *out = nullptr;
-        p->ev_used = used0;
-        p->ev_x_used = x0;
-        p->timing_eager = true;
-    }
-    return MCC_OK;
-}
-
 int launch_update_steps(mcc_problem* p, int n) {
     if (p->timing_window) p->win_steps += n;
-    bool eager = !p->use_graph || (p->timing && p->timing_eager);
-    hipGraphExec_t timed = nullptr;
-    if (!eager && p->timing) {
-        int rc = capture_timed(p, n, &timed);
-        if (rc) return rc;
-        eager = timed == nullptr;
-    } else if (!eager) {
+    // the split step's timing window runs eagerly (an event pair around the linearisation kernels of
+    // every step; HIP events recorded inside a captured graph carry no timestamps) behind k_delay,
+    // which keeps the GPU busy while the host enqueues the window, so the GPU then runs the steps
+    // back to back as it runs a graph's, without waiting for launches between kernels
+    const bool eager = !p->use_graph || p->timing;
+    if (!eager) {
         // every graph of this batch exists before the batch's helper starts: instantiating a 64-step
         // graph takes milliseconds, which the helper would otherwise spend polling for the first system
         for (int k = p->graph_sizes - 1, r = n; k >= 0; --k)
@@ -474,11 +447,7 @@ int launch_update_steps(mcc_problem* p, int n) {
         HIPCHK(mcc_launch_sinv_helper(warm_ctx(p), p->m, n, p->side));
     }
     int rc = MCC_OK;
-    if (timed) {
-        p->timed_execs.push_back(timed);
-        hipError_t e = hipGraphLaunch(timed, p->stream);
-        if (e != hipSuccess) rc = fail(MCC_EHIP, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
-    } else if (eager) {
+    if (eager) {
         for (int i = 0; i < n && rc == MCC_OK; ++i) rc = enqueue_step(p, 1, nullptr);
     } else {
         for (int k = p->graph_sizes - 1; k >= 0 && rc == MCC_OK; --k)
@@ -985,7 +954,6 @@ void mcc_destroy(mcc_problem* p) {
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
     for (auto e : p->ev_x) (void)hipEventDestroy(e);
     for (auto e : p->ev_marks) (void)hipEventDestroy(e);
-    for (auto g : p->timed_execs) (void)hipGraphExecDestroy(g);
     for (auto e : p->ev_win) if (e) (void)hipEventDestroy(e);
     if (p->comm) (void)ncclCommDestroy(p->comm);
     for (void* m : p->peer_mapped) (void)hipIpcCloseMemHandle(m);
@@ -1284,6 +1252,9 @@ int mcc_timing_begin(mcc_problem* p) {
         return MCC_OK;
     }
     p->timing = true;
+    // the GPU busy for ~5 ms (s_memrealtime) while the host enqueues the window's steps (a window of
+    // 100 split steps is ~600 API calls, ~2 ms)
+    HIPCHK(mcc_launch_delay(500000LL, p->stream));
     return MCC_OK;
 }
 
@@ -1302,8 +1273,6 @@ int mcc_timing_end(mcc_problem* p, double* lin_ms, double* step_ms, int* launche
         return MCC_OK;
     }
     HIPCHK(hipStreamSynchronize(p->stream));
-    for (auto g : p->timed_execs) (void)hipGraphExecDestroy(g);
-    p->timed_execs.clear();
     double lin = 0, st = 0;
     const int n = p->ev_used / 2;
     for (int i = 0; i < n; ++i) {
@@ -1351,11 +1320,6 @@ int mcc_timing_windows(mcc_problem* p, int n_windows, int steps, double* ms_per_
     }
     if (graph_launched) *graph_launched = p->use_graph ? 1 : 0;
     return MCC_OK;
-}
-
-int mcc_timing_mode(const mcc_problem* p) {
-    if (!p) return -1;
-    return p->timing_eager || !p->use_graph ? 0 : 1;
 }
 
 int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges) {

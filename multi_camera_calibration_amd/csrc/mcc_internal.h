@@ -296,6 +296,7 @@ hipError_t mcc_launch_peer_push(const mcc::PeerCtx& pc, const mcc::State* st, co
 hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s);
 hipError_t mcc_launch_sinv_helper(const mcc::WarmCtx& w, int m, int n_systems, hipStream_t s);
 hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
+hipError_t mcc_launch_delay(long long ticks, hipStream_t s);
 hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);
 hipError_t mcc_launch_peer_max(const mcc::PeerCtx& pc, mcc::State* st, double* v, hipStream_t s);
 hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s);

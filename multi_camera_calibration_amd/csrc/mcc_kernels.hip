@@ -3809,6 +3809,17 @@ hipError_t mcc_launch_peer_max(const PeerCtx& pc, State* st, double* v, hipStrea
     hipLaunchKernelGGL(k_peer_max, dim3(1), dim3(64), 0, s, pc, st, v);
     return hipGetLastError();
 }
+// one wave that waits `ticks` of the 100 MHz clock (vector-free, no memory traffic): the timing
+// window's head, so the host can enqueue the window before the GPU reaches it
+__global__ __launch_bounds__(64) void k_delay(long long ticks) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+}
+hipError_t mcc_launch_delay(long long ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, ticks);
+    return hipGetLastError();
+}
+
 hipError_t mcc_launch_backsub(const BacksubArgs& a, hipStream_t s) {
     if (a.n_photos > 0) hipLaunchKernelGGL(k_backsub, dim3((a.n_photos + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
