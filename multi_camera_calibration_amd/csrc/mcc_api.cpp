@@ -181,6 +181,7 @@ struct mcc_problem {
     bool poison = false;
     int poison_level = 0;
     bool peer_push = true;   // m > 30 with the peer transport: k_peer_push sends from many workgroups
+    int schur_one_level = 0; // k_schur's single hand-off level (m <= 30; MCC_SCHUR_ONE_LEVEL=0 restores two)
     int n_prep = 0, prep_lanes = 1;   // MCC_PREP_LANES=4: k_prep4 (measured slower at configs 3 and 5)
     // warm solve (m > 30 split step, MCC_WARM=0 turns it off): a resident helper kernel on a side
     // stream (one per batch of update steps) inverts each step's reduced system while the next step
@@ -371,6 +372,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     // final arriver exchanges and solves (no k_peer_push / k_solve launches)
     const bool split = rccl || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
+    sa.one_level = p->schur_one_level;
     sa.peer = peer_ctx(p, peer && !split);
     sa.solve = solve_ctx(p, do_update);
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
@@ -783,6 +785,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->n_items = (int)items.size();
     p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
+    p->schur_one_level = p->m <= 30 ? 1 : 0;
+    if (const char* f = std::getenv("MCC_SCHUR_ONE_LEVEL")) p->schur_one_level = p->m <= 30 && std::atoi(f) != 0;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;

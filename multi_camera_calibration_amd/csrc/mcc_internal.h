@@ -214,6 +214,7 @@ struct SchurArgs {
     const int* block_items;   // [nblk + 1]
     double* packed;
     int m, rank, fuse_solve;
+    int one_level;       // m <= 30: one hand-off level (schur_one_level) instead of items -> blocks -> norms
     SolveCtx solve;
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves

@@ -3193,6 +3193,98 @@ __device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, i
     }
 }
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
+
+// m <= 30 (at most 15 camera-pair blocks, a few dozen items): ONE hand-off level.  Every item and
+// norm chunk has written its partial (sc1) and takes one ticket; the last arriver sums each block's
+// items in item order -- the sums level 1 forms, so the bits are those of the two-level form -- and
+// places them straight into the solve's LDS matrix as well as the packed system (plain stores: the
+// peer exchange / all-reduce / host read it), instead of a second ticket over the blocks and a reload
+// of the packed system.  Round 3 measured the two levels at ~1.8 us each on config4's step tail.
+__device__ __noinline__ void schur_one_level(const SchurArgs& a) {
+    State* st = a.state;
+    const int tid = threadIdx.x;
+    if (!arrive_last_sc1(a.counter, (int)gridDim.x)) return;
+    STAMPP(a.stamps, 8, 2);
+    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* S = sm;          // m*m
+    double* r = sm + m * m;  // m
+    __shared__ double norms[2];
+    const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
+    if (tid < 2) {
+        const int w = tid;   // 0: normG2, 1: normX2 of the last update
+        const int iter = st->iter;
+        const double cn = w ? st->cam_normX2 : st->cam_normG2;
+        constexpr int B = 32;
+        double v = 0.0;
+        for (int k0 = a.n_items; k0 < (int)gridDim.x; k0 += B) {
+            double pv[B];
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                pv[u] = k0 + u < (int)gridDim.x ? ld_sc1(a.item_out + 48 * (size_t)(k0 + u) + w) : 0.0;
+#pragma unroll
+            for (int u = 0; u < B; ++u)
+                if (k0 + u < (int)gridDim.x) v += pv[u];
+        }
+        if (a.rank == 0) v += cn;
+        if (iter <= 0) v = 0.0;
+        v = photo_flag_norm(st, w, v);
+        norms[w] = v;
+        a.packed[ntri + 2 * m + w] = v;
+    }
+    for (int t = tid; t < a.nblk * 48; t += blockDim.x) {
+        const int blk = t / 48, e = t % 48;
+        const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
+        int b1 = 0;
+        while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
+        const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
+        if (e >= 36 && b1 != b2) continue;   // off-diagonal blocks: 36 entries, no r / JTE
+        double pv[kMaxItemsPerBlock];
+#pragma unroll
+        for (int q = 0; q < kMaxItemsPerBlock; ++q) pv[q] = q < nk ? ld_sc1(a.item_out + 48 * (size_t)(k0 + q) + e) : 0.0;
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? pv[q] : 0.0;
+        if (e < 36) {
+            const int ii = e / 6, jj = e % 6, i = 6 * b1 + ii, j = 6 * b2 + jj;
+            if (b1 != b2 || ii <= jj) {
+                a.packed[packed_index(i, j, m)] = v;
+                if (lds) {
+                    S[i * m + j] = v;
+                    S[j * m + i] = v;
+                }
+            }
+        } else {
+            const int w = (e - 36) / 6, i = 6 * b1 + (e - 36) % 6;
+            a.packed[ntri + w * m + i] = v;   // r (w = 0), JTE of the global block (w = 1)
+            if (lds && w == 0) r[i] = v;
+        }
+    }
+    if (!a.fuse_solve) return;
+    __syncthreads();   // the packed system and the norms (this workgroup's global stores and LDS)
+    if (a.peer.nranks > 0) {
+        // multi-GPU: the rank-ordered sum of every rank's system, then this rank solves it
+        if (!peer_exchange(a.peer, st, a.packed)) return;
+        for (int t = tid; t < ntri + m; t += blockDim.x) {
+            const double v = a.packed[t];
+            if (t < ntri) {
+                int i, j;
+                packed_ij(t, m, i, j);
+                S[i * m + j] = v;
+                S[j * m + i] = v;
+            } else {
+                r[t - ntri] = v;
+            }
+        }
+        if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
+        __syncthreads();
+    }
+    STAMPP(a.stamps, 8, 3);
+    SolveCtx sc = a.solve;
+    sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
+    solve_global<false>(sc, S, r, norms[0], norms[1]);
+    STAMPP(a.stamps, 8, 7);
+}
 #ifndef MCC_SCHUR_LOADS
 #define MCC_SCHUR_LOADS 32
 #endif
@@ -3233,7 +3325,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         if (tid < 48) {
             double t = part[0][tid];
             for (int c = 1; c < kSub; ++c) t += part[c][tid];
-            if (it.w & kItemSingle) schur_block_store(a, it.x, tid, 0.0 + t);   // as level 1 over one item
+            if ((it.w & kItemSingle) && !a.one_level) schur_block_store(a, it.x, tid, 0.0 + t);   // as level 1 over one item
             else st_sc1(a.item_out + 48 * (size_t)item + tid, t);
         }
     } else {
@@ -3251,6 +3343,10 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         }
     }
     STAMPP(a.stamps, 8, 1);
+    if (a.one_level) {
+        schur_one_level(a);
+        return;
+    }
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     // ---- level 1 (write-through hand-off, no fences): the last item of a camera-pair block sums
     // the block's items in item order and writes the block's entries of the packed system
