@@ -172,6 +172,8 @@ struct mcc_problem {
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
+    DevBuf<double> ssinv;              // m <= 30 warm solve: the previous system's inverse [m x m]
+    DevBuf<int> ssinv_ok;
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
     DevBuf<int> pgrp_ptr, pgrp_edge, gpair_ptr, gcon_ptr;
     DevBuf<int> prep_ptr, prep_edge;   // k_prep4's groups (three-kernel split step)
@@ -275,9 +277,16 @@ mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
 int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     using namespace mcc;
     const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
+    // the m <= 30 warm solve (k_group's spare workgroup inverts the previous step's system; k_schur
+    // refines with it): single GPU or the peer transport (with RCCL, k_solve solves)
+    const bool swarm = p->ssinv.p && (p->peer_on || !p->comm);
     if (p->poison) {
-        for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed})
-            if (b->p && b->n) HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
+        // (with the warm solve the packed system carries the previous step's system into the next
+        // step, like dg: it is an input of the step, not a hand-off inside it, and stays unpoisoned)
+        for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed, &p->ssinv})
+            if (b->p && b->n && !(swarm && b == &p->packed))
+                HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
+        if (swarm) HIPCHK(hipMemsetAsync(p->ssinv_ok.p, 0xFF, sizeof(int), p->stream));
         for (auto* b : {&p->erec, &p->echain, &p->eh})
             if (b->p && b->n) HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
         // 2: the negative control -- dg carries the previous solve into this step's photo update,
@@ -311,6 +320,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.photo_norm = p->photo_norm.p;
     la.stamps = p->stamps.p;
     la.fault_photo = p->fault_photo;
+    la.ssinv = swarm ? p->ssinv.p : nullptr;
+    la.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
     // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
     // split path: the packed system is summed by RCCL and solved by k_solve.  The peer transport
     // keeps one kernel per step: the final arriver exchanges with the peers and solves.
@@ -373,6 +384,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     const bool split = rccl || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
     sa.one_level = p->schur_one_level;
+    sa.ssinv = swarm ? p->ssinv.p : nullptr;
+    sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
     sa.peer = peer_ctx(p, peer && !split);
     sa.solve = solve_ctx(p, do_update);
     sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
@@ -915,6 +928,17 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (!p->fused && p->use_group && p->group_shmem > 160 * 1024)
         return bail(fail(MCC_EINVAL, "too many edges / Schur pairs of one photo group for k_group's LDS"));
     HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->use_group ? p->group_shmem : 0));
+    // m <= 30 on k_group -> k_schur (config4): the previous system's inverse from a spare k_group
+    // workgroup, refinement in k_schur's final solve (MCC_SMALL_WARM=0: the direct elimination only)
+    {
+        bool sw = !p->fused && p->use_group && p->schur_one_level;
+        if (const char* f = std::getenv("MCC_SMALL_WARM")) sw = sw && std::atoi(f) != 0;
+        if (sw) {
+            HIPC(p->ssinv.alloc((size_t)p->m * p->m));
+            HIPC(p->ssinv_ok.alloc(1));
+            HIPC(hipMemset(p->ssinv_ok.p, 0, sizeof(int)));
+        }
+    }
     p->warm = !p->fused && p->m > 30;
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
@@ -969,7 +993,7 @@ void mcc_destroy(mcc_problem* p) {
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->corner_err.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
-    p->erec.release(); p->echain.release(); p->eh.release();
+    p->erec.release(); p->echain.release(); p->eh.release(); p->ssinv.release(); p->ssinv_ok.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();

@@ -300,6 +300,10 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
+        if (!st->done) small_inverse(a);
+        return;
+    }
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
     const int done = st->done, pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update

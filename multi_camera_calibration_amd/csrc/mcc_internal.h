@@ -112,6 +112,9 @@ struct LinArgs {
     int n_prep, prep_lanes;  // prep_lanes: 4 (k_prep4) or 1 (k_prep, one lane per edge)
     int fault_photo;         // test (MCC_FAULT_PHOTO): this local photo's 6 x 6 block is reported not
                              // positive definite (its factor stays finite); -1 off
+    // m <= 30 warm solve: k_group's spare workgroup inverts the previous step's packed system
+    double* ssinv;           // [m x m] (null: off)
+    int* ssinv_ok;           // 1: ssinv holds the previous update step's inverse
 };
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
@@ -215,6 +218,8 @@ struct SchurArgs {
     double* packed;
     int m, rank, fuse_solve;
     int one_level;       // m <= 30: one hand-off level (schur_one_level) instead of items -> blocks -> norms
+    const double* ssinv; // m <= 30 warm solve: the previous system's inverse (k_group's spare workgroup)
+    const int* ssinv_ok;
     SolveCtx solve;
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves

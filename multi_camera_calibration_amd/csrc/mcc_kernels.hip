@@ -898,7 +898,7 @@ __device__ __forceinline__ double photo_flag_norm(State* st, int w, double v) {
 
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
-                                             const WarmCtx* warm = nullptr);
+                                             const WarmCtx* warm = nullptr, const double* Iv = nullptr);
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
@@ -3055,10 +3055,147 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
     }
 }
 
+// ---------------------------------------------------------------- the m <= 30 warm solve
+// The previous Gauss-Newton step's reduced system changes little by the next step, so its inverse is
+// a preconditioner good enough that iterative refinement reaches the elimination's accuracy in one or
+// two corrections -- a few 18 x 18 products on one wave against the 18-pivot register Gauss-Jordan's
+// chain of broadcasts (~5.4 k cycles).  The inverse is formed OFF the critical
+// path: k_group launches one spare workgroup beyond its groups (250 groups on 256 CUs at config4), which
+// inverts the packed system the previous step's k_schur left (gj_inverse_rows) while the groups
+// linearise; k_schur's final arriver reads it after the kernel boundary.  Every step forms it, so the
+// branch a step takes -- refinement, or the elimination when there is no previous system (an
+// optimisation's first step, a linearisation-only step) or the refinement does not converge -- is a
+// function of the systems alone, never of timing.
+
+// Gauss-Jordan on [S | I] by one wave, lane i owning row i of both halves (S from the packed upper
+// triangle in global memory); Sinv row i = (E row i) / d_i.  Returns false when a pivot is not > 0.
+template <int MM>
+__device__ bool gj_inverse_rows(const double* Pk, int m, int lane, double* out) {
+    const int li = lane < m ? lane : 0;
+    double row[MM], inv[MM];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        const int jj = j < m ? j : 0, lo = li < jj ? li : jj, hi = li < jj ? jj : li;
+        row[j] = Pk[lo * m - lo * (lo - 1) / 2 + (hi - lo)];
+        inv[j] = j == li ? 1.0 : 0.0;
+    }
+    double dii = 1.0;
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < MM; ++k) {
+        if (k >= m) break;
+        const double piv = readlane_f64(row[k], k);
+        bad |= !(piv > 0.0);
+        const double pv = piv > 0.0 ? piv : 1.0;
+        double ip = __builtin_amdgcn_rcp(pv);
+        ip = fma(ip, fma(-pv, ip, 1.0), ip);
+        if (lane == k) dii = pv;
+        const double f = lane == k ? 0.0 : row[k] * ip;
+        double pr[MM], pi[MM];   // the pivot row: S columns > k, inverse columns <= k (the rest are 0)
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            if (j > k && j < m) pr[j] = readlane_f64(row[j], k);
+            if (j <= k) pi[j] = readlane_f64(inv[j], k);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            if (j > k && j < m) row[j] -= f * pr[j];
+            if (j <= k) inv[j] -= f * pi[j];
+        }
+    }
+    const double id = 1.0 / dii;
+    if (lane < m)
+#pragma unroll
+        for (int j = 0; j < MM; ++j)
+            if (j < m) out[lane * m + j] = inv[j] * id;
+    return !bad;
+}
+__device__ bool gj_inverse_dispatch(const double* Pk, int m, int lane, double* out) {
+    switch (m) {
+        case 6: return gj_inverse_rows<6>(Pk, m, lane, out);
+        case 12: return gj_inverse_rows<12>(Pk, m, lane, out);
+        case 18: return gj_inverse_rows<18>(Pk, m, lane, out);
+        case 24: return gj_inverse_rows<24>(Pk, m, lane, out);
+        case 30: return gj_inverse_rows<30>(Pk, m, lane, out);
+        default: return false;
+    }
+}
+// k_group's spare workgroup: the inverse of the system the previous update step solved (st->pending:
+// it updated; otherwise, or when the system is not positive definite, ok = 0 and the next k_schur
+// eliminates directly).  Wave 0 only.
+__device__ void small_inverse(const LinArgs& a) {
+    const State* st = a.state;
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    int ok = 0;
+    if (st->pending) ok = gj_inverse_dispatch(a.packed, a.global_dim, lane, a.ssinv) ? 1 : 0;
+    if (lane == 0) a.ssinv_ok[0] = ok;
+}
+
+// x = S^-1 r by refinement with Iv (LDS, m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
+// equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i (the warm solve's test), at
+// most kWarmMaxIters corrections, each cutting the error fourfold.  On success r holds x.
+template <int MM>
+__device__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
+    const int li = lane < m ? lane : 0;
+    double srow[MM], irow[MM];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        srow[j] = j < m ? S[li * m + j] : 0.0;
+        irow[j] = j < m ? Iv[li * m + j] : 0.0;
+    }
+    const double rr = lane < m ? r[li] : 0.0;
+    double rv[MM];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) rv[j] = j < m ? r[j] : 0.0;
+    double x = 0.0;
+#pragma unroll
+    for (int j = 0; j < MM; ++j) x = fma(irow[j], rv[j], x);
+    constexpr double kTol = 64.0 * 1.1102230246251565e-16;
+    bool conv = false;
+    double qprev = 0.0;
+    for (int it = 0;; ++it) {
+        if (lane < 32) xw[lane] = lane < m ? x : 0.0;
+        wave_sync_lds();
+        double res = rr, sa = fabs(rr);
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            const double xj = xw[j];
+            res = fma(-srow[j], xj, res);
+            sa = fma(fabs(srow[j]), fabs(xj), sa);
+        }
+        const double q = lane < m ? (fabs(res) / fmax(sa, 1e-300)) : 0.0;
+        const double qm = wave_max(q == q ? q : 1.0);
+        conv = qm <= kTol;
+        if (conv || it >= kWarmMaxIters || (it > 0 && !(qm <= 0.25 * qprev))) break;
+        qprev = qm;
+        if (lane < 32) xw[32 + lane] = lane < m ? res : 0.0;
+        wave_sync_lds();
+        double dx = 0.0;
+#pragma unroll
+        for (int j = 0; j < MM; ++j) dx = fma(irow[j], xw[32 + j], dx);
+        x += dx;
+    }
+    wave_sync_lds();   // every lane has read r before it is overwritten
+    if (conv && lane < m) r[lane] = x;
+    return conv;
+}
+__device__ bool small_refine_dispatch(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
+    switch (m) {
+        case 6: return small_refine<6>(S, r, Iv, xw, m, lane);
+        case 12: return small_refine<12>(S, r, Iv, xw, m, lane);
+        case 18: return small_refine<18>(S, r, Iv, xw, m, lane);
+        case 24: return small_refine<24>(S, r, Iv, xw, m, lane);
+        case 30: return small_refine<30>(S, r, Iv, xw, m, lane);
+        default: return false;
+    }
+}
+
 // LARGE: m > 30 (k_solve only: the register-tiled elimination needs the whole workgroup's registers)
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
-                                             const WarmCtx* warm) {
+                                             const WarmCtx* warm, const double* Iv) {
     State* st = a.state;
     const int m = a.m, tid = threadIdx.x;
     __shared__ int stop, s_iter;
@@ -3103,7 +3240,10 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         // when the loop stops), so wave 1 runs it while wave 0 loads the state
         SSTAMP(a.stamps, 1, 64);
         if (tid == 64) s_bad_rows = 0;   // (this wave's own write below follows in program order)
-        gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
+        // with the previous system's inverse (k_schur, m <= 30): refinement, else / on failure the
+        // register Gauss-Jordan
+        __shared__ double s_xw[64];
+        if (!(Iv && small_refine_dispatch(S, r, Iv, s_xw, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
         SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();
@@ -3211,6 +3351,13 @@ __device__ __noinline__ void schur_one_level(const SchurArgs& a) {
     double* r = sm + m * m;  // m
     __shared__ double norms[2];
     const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
+    // the previous system's inverse from k_group's spare workgroup (issued with the partials' loads)
+    double* Iv = a.ssinv && a.fuse_solve ? sm + m * m + m : nullptr;
+    __shared__ int iv_ok;
+    if (Iv) {
+        if (tid == 0) iv_ok = a.ssinv_ok[0];
+        for (int t = tid; t < m * m; t += blockDim.x) Iv[t] = a.ssinv[t];
+    }
     if (tid < 2) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
         const int iter = st->iter;
@@ -3282,7 +3429,7 @@ __device__ __noinline__ void schur_one_level(const SchurArgs& a) {
     STAMPP(a.stamps, 8, 3);
     SolveCtx sc = a.solve;
     sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
-    solve_global<false>(sc, S, r, norms[0], norms[1]);
+    solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, Iv && iv_ok ? Iv : nullptr);
     STAMPP(a.stamps, 8, 7);
 }
 #ifndef MCC_SCHUR_LOADS
@@ -3778,7 +3925,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
 
 template <int MODEL, bool RATIONAL, bool PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
-    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), dim3(a.n_pgroups), dim3(kGroupRound * L), shmem, s, a);
+    // + the spare workgroup of the m <= 30 warm solve (small_inverse)
+    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), dim3(a.n_pgroups + (a.ssinv ? 1 : 0)),
+                       dim3(kGroupRound * L), shmem, s, a);
     return hipGetLastError();
 }
 template <int L>
@@ -3867,7 +4016,7 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, siz
 hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
     // LDS for the solve only when this launch solves (single GPU, m <= 30): the item workgroups
     // keep their occupancy
-    const size_t shm = a.fuse_solve ? (size_t)(a.m * a.m + a.m) * sizeof(double) : 0;
+    const size_t shm = a.fuse_solve ? (size_t)(a.m * a.m + a.m + (a.ssinv ? a.m * a.m : 0)) * sizeof(double) : 0;
     hipLaunchKernelGGL(k_schur, dim3(grid), dim3(256), shm, s, a);
     return hipGetLastError();
 }
