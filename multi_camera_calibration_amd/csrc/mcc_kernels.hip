@@ -890,10 +890,13 @@ __device__ __forceinline__ bool peer_exchange(const PeerCtx& pc, State* st, doub
 // ranks' replicated camera blocks never diverge (a rank-local stop would leave the other ranks
 // solving a system without its shard).  normX2 is a sum of squared float32 parameters, NaN only
 // when the state itself is, which is an error too.
-__device__ __forceinline__ double photo_flag_norm(State* st, int w, double v) {
-    if (w == 1 && (__hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kErrPhotoNotPD))
-        return __builtin_nan("");
-    return v;
+// err: State::error, loaded by the caller with its other loads (photo_error), so the flag costs no
+// round trip of its own on the final arriver's path
+__device__ __forceinline__ int photo_error(State* st) {
+    return __hip_atomic_load(&st->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double photo_flag_norm(int err, int w, double v) {
+    return w == 1 && (err & kErrPhotoNotPD) ? __builtin_nan("") : v;
 }
 
 template <bool LARGE>
@@ -1367,6 +1370,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         }
     };
     const bool peer = a.peer.nranks > 0;
+    const int err_now = photo_error(st);   // issued ahead of the group sums' loads
     for (int t = tid; t < Lc; t += blockDim.x) {
         double v = 0.0;
         v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
@@ -1377,7 +1381,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             } else {
                 v = 0.0;
             }
-            v = photo_flag_norm(st, w, v);
+            v = photo_flag_norm(err_now, w, v);
         }
         if (!peer) place(t, v);
         a.packed[t] = v;
@@ -3362,6 +3366,7 @@ __device__ __noinline__ void schur_one_level(const SchurArgs& a) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
         const int iter = st->iter;
         const double cn = w ? st->cam_normX2 : st->cam_normG2;
+        const int err_now = photo_error(st);
         constexpr int B = 32;
         double v = 0.0;
         for (int k0 = a.n_items; k0 < (int)gridDim.x; k0 += B) {
@@ -3375,7 +3380,7 @@ __device__ __noinline__ void schur_one_level(const SchurArgs& a) {
         }
         if (a.rank == 0) v += cn;
         if (iter <= 0) v = 0.0;
-        v = photo_flag_norm(st, w, v);
+        v = photo_flag_norm(err_now, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
     }
@@ -3525,6 +3530,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
         const int iter = st->iter;
         const double cn = w ? st->cam_normX2 : st->cam_normG2;
+        const int err_now = photo_error(st);
         constexpr int B = 32;
         double v = 0.0;
         for (int k0 = a.n_items; k0 < (int)gridDim.x; k0 += B) {
@@ -3538,7 +3544,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         }
         if (a.rank == 0) v += cn;
         if (iter <= 0) v = 0.0;
-        v = photo_flag_norm(st, w, v);
+        v = photo_flag_norm(err_now, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
     }
