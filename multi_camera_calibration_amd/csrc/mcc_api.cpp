@@ -931,7 +931,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // m <= 30 on k_group -> k_schur (config4): the previous system's inverse from a spare k_group
     // workgroup, refinement in k_schur's final solve (MCC_SMALL_WARM=0: the direct elimination only)
     {
-        bool sw = !p->fused && p->use_group && p->schur_one_level;
+        bool sw = !p->fused && p->use_group && p->schur_one_level &&
+                  p->group_shmem >= (size_t)2 * p->m * p->m * sizeof(double);   // the spare's [S | I] in LDS
         if (const char* f = std::getenv("MCC_SMALL_WARM")) sw = sw && std::atoi(f) != 0;
         if (sw) {
             HIPC(p->ssinv.alloc((size_t)p->m * p->m));

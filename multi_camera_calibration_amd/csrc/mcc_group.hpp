@@ -301,7 +301,8 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     State* st = a.state;
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
-        if (!st->done) small_inverse(a);
+        extern __shared__ __attribute__((aligned(16))) double smem_spare[];
+        if (!st->done) small_inverse(a, smem_spare);
         return;
     }
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)

@@ -3071,91 +3071,71 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 // optimisation's first step, a linearisation-only step) or the refinement does not converge -- is a
 // function of the systems alone, never of timing.
 
-// Gauss-Jordan on [S | I] by one wave, lane i owning row i of both halves (S from the packed upper
-// triangle in global memory); Sinv row i = (E row i) / d_i.  Returns false when a pivot is not > 0.
-template <int MM>
-__device__ bool gj_inverse_rows(const double* Pk, int m, int lane, double* out) {
-    const int li = lane < m ? lane : 0;
-    double row[MM], inv[MM];
-#pragma unroll
-    for (int j = 0; j < MM; ++j) {
-        const int jj = j < m ? j : 0, lo = li < jj ? li : jj, hi = li < jj ? jj : li;
-        row[j] = Pk[lo * m - lo * (lo - 1) / 2 + (hi - lo)];
-        inv[j] = j == li ? 1.0 : 0.0;
-    }
-    double dii = 1.0;
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < MM; ++k) {
-        if (k >= m) break;
-        const double piv = readlane_f64(row[k], k);
-        bad |= !(piv > 0.0);
-        const double pv = piv > 0.0 ? piv : 1.0;
-        double ip = __builtin_amdgcn_rcp(pv);
-        ip = fma(ip, fma(-pv, ip, 1.0), ip);
-        if (lane == k) dii = pv;
-        const double f = lane == k ? 0.0 : row[k] * ip;
-        double pr[MM], pi[MM];   // the pivot row: S columns > k, inverse columns <= k (the rest are 0)
-#pragma unroll
-        for (int j = 0; j < MM; ++j) {
-            if (j > k && j < m) pr[j] = readlane_f64(row[j], k);
-            if (j <= k) pi[j] = readlane_f64(inv[j], k);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < MM; ++j) {
-            if (j > k && j < m) row[j] -= f * pr[j];
-            if (j <= k) inv[j] -= f * pi[j];
-        }
-    }
-    const double id = 1.0 / dii;
-    if (lane < m)
-#pragma unroll
-        for (int j = 0; j < MM; ++j)
-            if (j < m) out[lane * m + j] = inv[j] * id;
-    return !bad;
-}
-__device__ bool gj_inverse_dispatch(const double* Pk, int m, int lane, double* out) {
-    switch (m) {
-        case 6: return gj_inverse_rows<6>(Pk, m, lane, out);
-        case 12: return gj_inverse_rows<12>(Pk, m, lane, out);
-        case 18: return gj_inverse_rows<18>(Pk, m, lane, out);
-        case 24: return gj_inverse_rows<24>(Pk, m, lane, out);
-        case 30: return gj_inverse_rows<30>(Pk, m, lane, out);
-        default: return false;
-    }
-}
-// k_group's spare workgroup: the inverse of the system the previous update step solved (st->pending:
-// it updated; otherwise, or when the system is not positive definite, ok = 0 and the next k_schur
-// eliminates directly).  Wave 0 only.
-__device__ void small_inverse(const LinArgs& a) {
+// Gauss-Jordan on [S | I] in LDS by the whole workgroup (S from the packed upper triangle in global
+// memory; thread-per-element updates, two barriers per pivot: ~2 us at m = 18, off the critical path,
+// and no register arrays that would raise k_group's register pressure); Sinv row i = (E row i) / d_i.
+// ok = 0 when a pivot is not > 0.
+__device__ __noinline__ void small_inverse(const LinArgs& a, double* A) {
     const State* st = a.state;
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x;
-    int ok = 0;
-    if (st->pending) ok = gj_inverse_dispatch(a.packed, a.global_dim, lane, a.ssinv) ? 1 : 0;
-    if (lane == 0) a.ssinv_ok[0] = ok;
+    const int tid = threadIdx.x, nt = blockDim.x, m = a.global_dim, W = 2 * m;
+    __shared__ int ok_s;
+    if (!st->pending) {   // no update step before this one: no system to precondition with
+        if (tid == 0) a.ssinv_ok[0] = 0;
+        return;
+    }
+    for (int t = tid; t < m * W; t += nt) {
+        const int i = t / W, j = t % W;
+        double v;
+        if (j < m) {
+            const int lo = i < j ? i : j, hi = i < j ? j : i;
+            v = a.packed[lo * m - lo * (lo - 1) / 2 + (hi - lo)];
+        } else {
+            v = j - m == i ? 1.0 : 0.0;
+        }
+        A[t] = v;
+    }
+    if (tid == 0) ok_s = 1;
+    __syncthreads();
+    for (int k = 0; k < m; ++k) {
+        const double piv = A[k * W + k];
+        if (!(piv > 0.0)) {
+            if (tid == 0) ok_s = 0;
+            break;   // uniform: every thread read the same pivot
+        }
+        const double ip = 1.0 / piv;
+        double nv[8];   // <= 8 elements per thread: 30 x 60 over 256 threads (k_group's 16-lane form)
+        int nn = 0;
+        for (int t = tid; t < m * W; t += nt, ++nn) {
+            const int i = t / W, j = t % W;
+            nv[nn & 7] = i == k ? A[t] : A[t] - A[i * W + k] * ip * A[k * W + j];
+        }
+        __syncthreads();
+        nn = 0;
+        for (int t = tid; t < m * W; t += nt, ++nn) A[t] = nv[nn & 7];
+        __syncthreads();
+    }
+    __syncthreads();
+    const bool ok = ok_s != 0;
+    if (ok)
+        for (int t = tid; t < m * m; t += nt) {
+            const int i = t / m, j = t % m;
+            a.ssinv[t] = A[i * W + m + j] / A[i * W + i];
+        }
+    if (tid == 0) a.ssinv_ok[0] = ok ? 1 : 0;
 }
 
 // x = S^-1 r by refinement with Iv (LDS, m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
 // equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i (the warm solve's test), at
-// most kWarmMaxIters corrections, each cutting the error fourfold.  On success r holds x.
-template <int MM>
-__device__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
+// most kWarmMaxIters corrections, each cutting the error fourfold.  S, Iv and the vectors are read
+// from LDS as they are used (few registers: the solve's wave runs inside k_schur's final arriver).
+// On success r holds x.
+__device__ __noinline__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
     const int li = lane < m ? lane : 0;
-    double srow[MM], irow[MM];
-#pragma unroll
-    for (int j = 0; j < MM; ++j) {
-        srow[j] = j < m ? S[li * m + j] : 0.0;
-        irow[j] = j < m ? Iv[li * m + j] : 0.0;
-    }
+    const double* Sr = S + li * m;
+    const double* Ir = Iv + li * m;
     const double rr = lane < m ? r[li] : 0.0;
-    double rv[MM];
-#pragma unroll
-    for (int j = 0; j < MM; ++j) rv[j] = j < m ? r[j] : 0.0;
     double x = 0.0;
-#pragma unroll
-    for (int j = 0; j < MM; ++j) x = fma(irow[j], rv[j], x);
+    for (int j = 0; j < m; ++j) x = fma(Ir[j], r[j], x);
     constexpr double kTol = 64.0 * 1.1102230246251565e-16;
     bool conv = false;
     double qprev = 0.0;
@@ -3163,11 +3143,10 @@ __device__ bool small_refine(const double* S, double* r, const double* Iv, doubl
         if (lane < 32) xw[lane] = lane < m ? x : 0.0;
         wave_sync_lds();
         double res = rr, sa = fabs(rr);
-#pragma unroll
-        for (int j = 0; j < MM; ++j) {
-            const double xj = xw[j];
-            res = fma(-srow[j], xj, res);
-            sa = fma(fabs(srow[j]), fabs(xj), sa);
+        for (int j = 0; j < m; ++j) {
+            const double sj = Sr[j], xj = xw[j];
+            res = fma(-sj, xj, res);
+            sa = fma(fabs(sj), fabs(xj), sa);
         }
         const double q = lane < m ? (fabs(res) / fmax(sa, 1e-300)) : 0.0;
         const double qm = wave_max(q == q ? q : 1.0);
@@ -3177,23 +3156,12 @@ __device__ bool small_refine(const double* S, double* r, const double* Iv, doubl
         if (lane < 32) xw[32 + lane] = lane < m ? res : 0.0;
         wave_sync_lds();
         double dx = 0.0;
-#pragma unroll
-        for (int j = 0; j < MM; ++j) dx = fma(irow[j], xw[32 + j], dx);
+        for (int j = 0; j < m; ++j) dx = fma(Ir[j], xw[32 + j], dx);
         x += dx;
     }
     wave_sync_lds();   // every lane has read r before it is overwritten
     if (conv && lane < m) r[lane] = x;
     return conv;
-}
-__device__ bool small_refine_dispatch(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
-    switch (m) {
-        case 6: return small_refine<6>(S, r, Iv, xw, m, lane);
-        case 12: return small_refine<12>(S, r, Iv, xw, m, lane);
-        case 18: return small_refine<18>(S, r, Iv, xw, m, lane);
-        case 24: return small_refine<24>(S, r, Iv, xw, m, lane);
-        case 30: return small_refine<30>(S, r, Iv, xw, m, lane);
-        default: return false;
-    }
 }
 
 // LARGE: m > 30 (k_solve only: the register-tiled elimination needs the whole workgroup's registers)
@@ -3247,7 +3215,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         // with the previous system's inverse (k_schur, m <= 30): refinement, else / on failure the
         // register Gauss-Jordan
         __shared__ double s_xw[64];
-        if (!(Iv && small_refine_dispatch(S, r, Iv, s_xw, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
+        if (!(Iv && small_refine(S, r, Iv, s_xw, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
         SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();
