@@ -3075,7 +3075,7 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 // memory; thread-per-element updates, two barriers per pivot: ~2 us at m = 18, off the critical path,
 // and no register arrays that would raise k_group's register pressure); Sinv row i = (E row i) / d_i.
 // ok = 0 when a pivot is not > 0.
-__device__ __noinline__ void small_inverse(const LinArgs& a, double* A) {
+__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
     const State* st = a.state;
     const int tid = threadIdx.x, nt = blockDim.x, m = a.global_dim, W = 2 * m;
     __shared__ int ok_s;
@@ -3129,7 +3129,7 @@ __device__ __noinline__ void small_inverse(const LinArgs& a, double* A) {
 // most kWarmMaxIters corrections, each cutting the error fourfold.  S, Iv and the vectors are read
 // from LDS as they are used (few registers: the solve's wave runs inside k_schur's final arriver).
 // On success r holds x.
-__device__ __noinline__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
+__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
     const int li = lane < m ? lane : 0;
     const double* Sr = S + li * m;
     const double* Ir = Iv + li * m;
@@ -3312,7 +3312,7 @@ constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <
 // places them straight into the solve's LDS matrix as well as the packed system (plain stores: the
 // peer exchange / all-reduce / host read it), instead of a second ticket over the blocks and a reload
 // of the packed system.  Round 3 measured the two levels at ~1.8 us each on config4's step tail.
-__device__ __noinline__ void schur_one_level(const SchurArgs& a) {
+__device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     State* st = a.state;
     const int tid = threadIdx.x;
     if (!arrive_last_sc1(a.counter, (int)gridDim.x)) return;

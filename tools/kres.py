@@ -17,7 +17,8 @@ for line in out.splitlines():
         cur = {"name": m.group(1)}
         rows.append(cur)
         continue
-    for key in ("VGPRs", "AGPRs", "SGPRs Spill", "VGPRs Spill", "Occupancy \\[waves/SIMD\\]", "LDS Size \\[bytes/block\\]"):
+    for key in ("VGPRs", "AGPRs", "SGPRs Spill", "VGPRs Spill", "Occupancy \\[waves/SIMD\\]", "LDS Size \\[bytes/block\\]",
+                "ScratchSize \\[bytes/lane\\]"):
         m = re.search(r"\s" + key + r": (\d+)", line)
         if m and cur is not None:
             cur[key.split(" [")[0].replace("\\", "")] = int(m.group(1))
@@ -25,4 +26,4 @@ flt = sys.argv[1] if len(sys.argv) > 1 else ""
 for r in rows:
     if flt in r["name"]:
         print(f"{r['name'][:70]:70s} VGPR {r.get('VGPRs', '?'):>4} AGPR {r.get('AGPRs', '?'):>4} "
-              f"vspill {r.get('VGPRs Spill', '?'):>4} sspill {r.get('SGPRs Spill', '?'):>4} occ {r.get('Occupancy', '?')}")
+              f"vspill {r.get('VGPRs Spill', '?'):>4} sspill {r.get('SGPRs Spill', '?'):>4} scratch {r.get('ScratchSize', '?')}")
