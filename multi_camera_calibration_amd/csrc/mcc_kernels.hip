@@ -2888,7 +2888,7 @@ __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigne
     *e_s = e;
 }
 __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, int m, int* err, const WarmStage& ws,
-                            int use, unsigned e, int* bad_lds) {
+                            int use, unsigned e, int* bad_lds, long long* stp = nullptr) {
     const int tid = threadIdx.x, M = 16 * ((m + 15) / 16), n2 = warm_lc2(m);
     double* Pk = x + kWarmN;                         // staged packed [S | r] (x: kWarmN doubles)
     double* Iv = Pk + 2 * n2;                        // staged S_t^-1
@@ -2901,6 +2901,7 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
             st_sys_x2(w.sprev + 2 * q, ws.v[u].x, ws.v[u].y);
         }
     }
+    SSTAMP(stp, 8, 0);   // [S | r] staged, the sprev stores issued
     bool solved = false;
     if (use > 0) {
         // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
@@ -2926,12 +2927,16 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
             }
         }
         lds_barrier();
+        SSTAMP(stp, 9, 0);   // S_t^-1 in LDS, the rows of S_{t+1} gathered
         solved = warm_refine(Sr, Iv, Pk, x, work, m, w.stats);
+        SSTAMP(stp, 10, 0);   // refined
     }
     if (!solved) gj_blocked(packed, x, x + M, x + M + M * (M + 1), m, err, nullptr, bad_lds);
+    SSTAMP(stp, 11, 0);
     // publish this step's system (its sprev stores drained) for the helper
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    SSTAMP(stp, 12, 0);   // sprev drained
     if (tid == 0) st_sys_u32(w.sync, e + 1u);
 }
 
@@ -3234,7 +3239,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     SSTAMP(a.stamps, 4, 0);
     if (LARGE) {   // S is the packed system itself (global); r (LDS) is followed by the block work area
         const int M = 16 * ((m + 15) / 16);
-        if (wrm) warm_finish(S, *warm, r, m, &st->error, ws, s_use, s_ep, &s_bad);
+        if (wrm) warm_finish(S, *warm, r, m, &st->error, ws, s_use, s_ep, &s_bad, a.stamps);
         else gj_blocked(S, r, r + M, r + M + M * (M + 1), m, &st->error, nullptr, &s_bad);
     }
     SSTAMP(a.stamps, 5, 0);
