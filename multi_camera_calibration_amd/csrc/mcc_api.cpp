@@ -191,7 +191,8 @@ struct mcc_problem {
     bool warm = false;
     hipStream_t side = nullptr;      // the helper's stream
     double* sinv = nullptr;          // [M x M] (ordinary memory)
-    double* sprev = nullptr;         // uncached: packed [S | r]
+    double* prev2 = nullptr;         // uncached: [2][prev_stride] k_schur's copies of [S | r] (iteration parity)
+    int prev_stride = 0;
     unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
@@ -258,7 +259,8 @@ mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
 }
 
 mcc::WarmCtx warm_ctx(mcc_problem* p) {
-    return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->sprev, p->wsync, p->warm_stats.p,
+    const int copy_prev = (p->comm || p->peer_on) ? 1 : 0;   // sharded: k_solve copies the summed system
+    return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->prev2, p->prev_stride, copy_prev, p->wsync, p->warm_stats.p,
                         p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks};
 }
 
@@ -384,6 +386,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     const bool split = rccl || p->m > 30;
     sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
     sa.one_level = p->schur_one_level;
+    sa.prev2 = p->warm && do_update && !p->comm && !p->peer_on ? p->prev2 : nullptr;   // single GPU
+    sa.prev_stride = p->prev_stride;
     sa.ssinv = swarm ? p->ssinv.p : nullptr;
     sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
     sa.peer = peer_ctx(p, peer && !split);
@@ -959,7 +963,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (p->warm) {
         const size_t M = 16 * (size_t)((p->m + 15) / 16);
         HIPC(hipMalloc((void**)&p->sinv, M * M * sizeof(double)));   // cached: the helper releases it, k_solve reads it in a later launch
-        HIPC(hipExtMallocWithFlags((void**)&p->sprev, ((size_t)p->ntri + p->m + 2) * sizeof(double), hipDeviceMallocUncached));
+        p->prev_stride = (p->ntri + p->m + 1) & ~1;
+        HIPC(hipExtMallocWithFlags((void**)&p->prev2, 2 * (size_t)p->prev_stride * sizeof(double), hipDeviceMallocUncached));
         HIPC(hipExtMallocWithFlags((void**)&p->wsync, 4 * sizeof(unsigned), hipDeviceMallocUncached));
         HIPC(hipMemset(p->wsync, 0, 4 * sizeof(unsigned)));
         HIPC(p->warm_stats.alloc(5));
@@ -978,7 +983,7 @@ void mcc_destroy(mcc_problem* p) {
     const bool side_drained = p->side && hipStreamSynchronize(p->side) == hipSuccess;
     const bool drained = p->stream && hipStreamSynchronize(p->stream) == hipSuccess;
     if (p->sinv) (void)hipFree(p->sinv);
-    if (p->sprev) (void)hipFree(p->sprev);
+    if (p->prev2) (void)hipFree(p->prev2);
     if (p->wsync) (void)hipFree(p->wsync);
     p->warm_stats.release();
     for (auto& g : p->gexec)

@@ -223,6 +223,8 @@ struct SchurArgs {
     SolveCtx solve;
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
+    double* prev2;       // m > 30 warm solve: [2][prev_stride] copy of [S | r] for the helper (null: off)
+    int prev_stride;
 };
 
 // The m > 30 solve with the previous step's inverse (the "warm" solve, solve_large in
@@ -232,6 +234,11 @@ struct SchurArgs {
 // when the refinement does not converge within kWarmMaxIters corrections.  sinv_ok_sys, sprev and
 // sync are uncached device memory (the helper and the k_solve launches hand them over while both
 // run); sinv is ordinary memory, written back by the helper (agent release) before its epoch.
+// The system itself reaches the helper through prev2: k_schur writes [S | r] to prev2[iter & 1] beside
+// the packed system (one more write-through store per entry, spread over the block workgroups), and
+// k_solve publishes the epoch e + 1 (iteration e solved) as soon as it holds S_t^-1 in LDS -- no copy
+// or store drain of its own.  The double buffer is safe: the step that writes prev2[iter & 1] again
+// starts after the next k_solve, which waited for the helper to invert (and so to read) this one.
 // Which algorithm a step takes depends only on the systems (the epoch count, the helper's PD flag,
 // the refinement's convergence), never on timing: k_solve always waits for the previous system's
 // inverse, and a helper that does not deliver within wait_ticks fails the step (error bit 3,
@@ -239,7 +246,10 @@ struct SchurArgs {
 struct WarmCtx {
     double* sinv;            // [M x M] (M = 16 ceil(m / 16), row-major) the helper's inverse
     int* sinv_ok_sys;        // the helper's elimination found the system positive definite
-    double* sprev;           // [packed [S | r] rounded up to even] the last solved system, for the helper
+    double* prev2;           // [2][prev_stride] uncached: the copy of [S | r] per iteration parity
+    int prev_stride;         // packed [S | r] rounded up to even
+    int copy_prev;           // 1: k_solve writes the copy (sharded: the rank-summed system exists only
+                             // after the exchange); 0: k_schur wrote it (single GPU)
     unsigned* sync;          // [3] epochs: systems published by k_solve, systems inverted by the helper; stop
     long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), waited for the helper
     int poison;              // test (MCC_WARM_POISON=1): the helper publishes a NaN inverse, so every

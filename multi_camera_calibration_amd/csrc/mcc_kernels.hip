@@ -2893,15 +2893,21 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     double* Pk = x + kWarmN;                         // staged packed [S | r] (x: kWarmN doubles)
     double* Iv = Pk + 2 * n2;                        // staged S_t^-1
     double* work = Iv + (size_t)M * (M + 2);
+    double* prev = w.prev2 + (size_t)(e & 1u) * w.prev_stride;   // iteration e's copy
 #pragma unroll
     for (int u = 0; u < kWarmPer; ++u) {
         const int q = u * (int)blockDim.x + tid;
         if (q < n2) {
             reinterpret_cast<double2*>(Pk)[q] = ws.v[u];
-            st_sys_x2(w.sprev + 2 * q, ws.v[u].x, ws.v[u].y);
+            if (w.copy_prev) st_sys_x2(prev + 2 * q, ws.v[u].x, ws.v[u].y);   // sharded: the summed system
         }
     }
-    SSTAMP(stp, 8, 0);   // [S | r] staged, the sprev stores issued
+    SSTAMP(stp, 8, 0);   // [S | r] staged
+    // single GPU: publish this step's system (k_schur left it in prev2[e & 1]) for the helper as soon
+    // as this k_solve no longer needs S_t^-1 -- at once on the direct path, after S_t^-1 is in LDS
+    // otherwise; sharded: after this k_solve's own copy has drained (at the end)
+    const bool early = !w.copy_prev;
+    if (early && use <= 0 && tid == 0) st_sys_u32(w.sync, e + 1u);
     bool solved = false;
     if (use > 0) {
         // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
@@ -2927,17 +2933,18 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
             }
         }
         lds_barrier();
+        if (early && tid == 0) st_sys_u32(w.sync, e + 1u);
         SSTAMP(stp, 9, 0);   // S_t^-1 in LDS, the rows of S_{t+1} gathered
         solved = warm_refine(Sr, Iv, Pk, x, work, m, w.stats);
         SSTAMP(stp, 10, 0);   // refined
     }
     if (!solved) gj_blocked(packed, x, x + M, x + M + M * (M + 1), m, err, nullptr, bad_lds);
     SSTAMP(stp, 11, 0);
-    // publish this step's system (its sprev stores drained) for the helper
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    SSTAMP(stp, 12, 0);   // sprev drained
-    if (tid == 0) st_sys_u32(w.sync, e + 1u);
+    if (!early) {   // sharded: publish after the copy's stores drained
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (tid == 0) st_sys_u32(w.sync, e + 1u);
+    }
 }
 
 // In-place blocked Gauss-Jordan inverse of the padded SPD system in LDS (A: M x M, stride ld = M + 1,
@@ -3014,10 +3021,12 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         __syncthreads();
         if (quit_s) return;
         const unsigned e = ep_s;
-        // sprev -> the full symmetric matrix in LDS (padding: identity)
+        // system e (solved by the update step whose iteration counter was e - 1: k_schur wrote it to
+        // prev2[(e - 1) & 1]) -> the full symmetric matrix in LDS (padding: identity)
         const int ntri = m * (m + 1) / 2, n2 = (ntri + 1) / 2;
+        const double* src = w.prev2 + (size_t)((e - 1u) & 1u) * w.prev_stride;
         for (int q = tid; q < n2; q += blockDim.x) {
-            const double2 v = ld_sys_x2(w.sprev + 2 * q);
+            const double2 v = ld_sys_x2(src + 2 * q);
             for (int h = 0; h < 2; ++h) {
                 const int t = 2 * q + h;
                 if (t < ntri) {
@@ -3296,17 +3305,23 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 // (One last-arriver assembling every block alone took ~56 us at m = 90.)
 constexpr int kSub = 5;
 // entry tid < 48 of camera-pair block blk's sum -> the packed system (write-through)
-__device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, int tid, double v) {
+// prev: the warm solve's copy of [S | r] for the helper (prev2[iteration & 1], uncached), or null
+__device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, int tid, double v, double* prev) {
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     int b1 = 0;
     while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
     const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
     if (tid < 36) {
         const int ii = tid / 6, jj = tid % 6;
-        if (b1 != b2 || ii <= jj) st_sc1(a.packed + packed_index(6 * b1 + ii, 6 * b2 + jj, m), v);
+        if (b1 != b2 || ii <= jj) {
+            const int k = packed_index(6 * b1 + ii, 6 * b2 + jj, m);
+            st_sc1(a.packed + k, v);
+            if (prev) st_sc1(prev + k, v);
+        }
     } else if (b1 == b2) {
         const int w = (tid - 36) / 6, i = 6 * b1 + (tid - 36) % 6;
         st_sc1(a.packed + ntri + w * m + i, v);   // r (w = 0), JTE of the global block (w = 1)
+        if (prev && w == 0) st_sc1(prev + ntri + i, v);
     }
 }
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
@@ -3416,6 +3431,8 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
 __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
+    // the warm solve's copy of this step's [S | r] (m > 30): prev2[iteration & 1] (same cache line as done)
+    double* prev = a.prev2 ? a.prev2 + (size_t)(st->iter & 1) * a.prev_stride : nullptr;
     STAMPP(a.stamps, 8, 0);
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
@@ -3450,7 +3467,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
         if (tid < 48) {
             double t = part[0][tid];
             for (int c = 1; c < kSub; ++c) t += part[c][tid];
-            if ((it.w & kItemSingle) && !a.one_level) schur_block_store(a, it.x, tid, 0.0 + t);   // as level 1 over one item
+            if ((it.w & kItemSingle) && !a.one_level) schur_block_store(a, it.x, tid, 0.0 + t, prev);   // as level 1 over one item
             else st_sc1(a.item_out + 48 * (size_t)item + tid, t);
         }
     } else {
@@ -3487,7 +3504,7 @@ __global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
             double v = 0.0;
 #pragma unroll
             for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? pv[q] : 0.0;
-            schur_block_store(a, blk, tid, v);
+            schur_block_store(a, blk, tid, v, prev);
         }
     }
     STAMPP(a.stamps, 8, 2);
