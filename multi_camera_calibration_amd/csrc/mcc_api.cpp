@@ -806,8 +806,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     p->n_items = (int)items.size();
     p->n_pairs = n_slots;
     p->n_norm_chunks = (V + 255) / 256;
-    p->schur_one_level = p->m <= 30 ? 1 : 0;
-    if (const char* f = std::getenv("MCC_SCHUR_ONE_LEVEL")) p->schur_one_level = p->m <= 30 && std::atoi(f) != 0;
+    // one hand-off level (m <= 30) while the final arriver loads everything in one batch
+    const bool one_fits = p->m <= 30 && 48 * (p->n_items + p->n_norm_chunks) + p->m * p->m <= mcc::kSchurOneLevelLoads * 256;
+    p->schur_one_level = one_fits ? 1 : 0;
+    if (const char* f = std::getenv("MCC_SCHUR_ONE_LEVEL")) p->schur_one_level = one_fits && std::atoi(f) != 0;
     if (p->m > 128) return bail(fail(MCC_EINVAL, "global block larger than 128 parameters (22 cameras)"));
     p->group_size = std::max(1, (int)std::ceil(std::sqrt((double)std::max(V, 1))));
     p->n_groups = (std::max(V, 1) + p->group_size - 1) / p->group_size;

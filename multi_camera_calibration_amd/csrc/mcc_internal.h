@@ -204,6 +204,22 @@ __host__ __device__ inline size_t prep_lds_bytes(int C, bool back) {
     return (size_t)L.ndoubles * 8 + (size_t)L.nints * 4;
 }
 
+// k_schur's dynamic LDS (doubles): the final arriver's S (m x m) and r (m) when the launch solves
+// (fuse_solve), the m <= 30 warm solve's inverse (m x m, ssinv), and with one hand-off level the copy
+// of every workgroup's partials (48 per item or norm chunk, grid) followed by the block ranges (nblk + 1
+// ints) -- all of them loaded in one round trip
+__host__ __device__ inline size_t schur_items_offset(int m, int fuse, int ssinv) {
+    return fuse ? (size_t)m * m + m + (ssinv ? (size_t)m * m : 0) : 0;
+}
+__host__ __device__ inline size_t schur_lds_bytes(int m, int fuse, int ssinv, int one_level, int grid, int nblk) {
+    size_t d = schur_items_offset(m, fuse, ssinv);
+    if (one_level) d += 48 * (size_t)grid + (nblk + 2) / 2;
+    return d * sizeof(double);
+}
+// one hand-off level only while the final arriver's copy is one batch of loads: 48 grid + m^2 <=
+// kSchurOneLevelLoads x 256 (k_schur's threads)
+constexpr int kSchurOneLevelLoads = 16;
+
 struct SchurArgs {
     State* state;
     const int4* items;   // {camera-pair block, first slot's offset in doubles, slot count, slot size 48 | 36}

@@ -3304,6 +3304,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 // last of the blocks and norm chunks adds the norms and, with fuse_solve (single GPU), solves.
 // (One last-arriver assembling every block alone took ~56 us at m = 90.)
 constexpr int kSub = 5;
+constexpr int kSchurThreads = 256;   // k_schur's workgroup (mcc_launch_schur)
 // entry tid < 48 of camera-pair block blk's sum -> the packed system (write-through)
 // prev: the warm solve's copy of [S | r] for the helper (prev2[iteration & 1], uncached), or null
 __device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, int tid, double v, double* prev) {
@@ -3332,6 +3333,11 @@ constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <
 // places them straight into the solve's LDS matrix as well as the packed system (plain stores: the
 // peer exchange / all-reduce / host read it), instead of a second ticket over the blocks and a reload
 // of the packed system.  Round 3 measured the two levels at ~1.8 us each on config4's step tail.
+// Every value the final arriver needs -- the partials of all items and norm chunks, the block ranges,
+// the warm solve's inverse, the state -- is loaded in ONE round trip into LDS (batches of
+// independent unconditional loads: a load under a per-item condition, or a loop whose stores wait
+// on its loads, costs a round trip per load or iteration: 5 us at config4 in the first form), and
+// the sums are formed from LDS.
 __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     State* st = a.state;
     const int tid = threadIdx.x;
@@ -3343,48 +3349,59 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     double* r = sm + m * m;  // m
     __shared__ double norms[2];
     const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
-    // the previous system's inverse from k_group's spare workgroup (issued with the partials' loads)
+    // the previous system's inverse from k_group's spare workgroup
     double* Iv = a.ssinv && a.fuse_solve ? sm + m * m + m : nullptr;
+    double* itm = sm + schur_items_offset(m, a.fuse_solve, a.ssinv != nullptr);   // [grid][48]
+    int* sbi = reinterpret_cast<int*>(itm + 48 * (size_t)gridDim.x);                // [nblk + 1]
     __shared__ int iv_ok;
-    if (Iv) {
-        if (tid == 0) iv_ok = a.ssinv_ok[0];
-        for (int t = tid; t < m * m; t += blockDim.x) Iv[t] = a.ssinv[t];
+    // ---- the round trip: every load unconditional (uniform words as scalar loads, no branch for
+    // the compiler to wait at), consumed only after the barrier
+    const int bi = a.block_items[tid < a.nblk ? tid : a.nblk];
+    const int iter = st->iter;
+    const double cn0 = st->cam_normG2, cn1 = st->cam_normX2;
+    const int err_now = photo_error(st);
+    const int ivok = Iv ? a.ssinv_ok[0] : 0;
+    {
+        // one batch, no loop (a loop's header waits for the previous iteration's loads, and so for
+        // the state loads above): the host keeps 48 grid + m^2 <= kSchurOneLevelLoads * 256
+        const int nI = 48 * (int)gridDim.x, nV = Iv ? m * m : 0, n = nI + nV;
+        constexpr int U = kSchurOneLevelLoads;
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int t = u * kSchurThreads + tid;
+            t = t < n ? t : n - 1;
+            v[u] = ld_sc1(t < nI ? a.item_out + t : a.ssinv + (t - nI));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = u * kSchurThreads + tid;
+            if (t < nI) itm[t] = v[u];
+            else if (t < n) Iv[t - nI] = v[u];
+        }
     }
+    if (tid <= a.nblk) sbi[tid] = bi;
+    if (tid == 0) iv_ok = ivok;
+    __syncthreads();
     if (tid < 2) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
-        const int iter = st->iter;
-        const double cn = w ? st->cam_normX2 : st->cam_normG2;
-        const int err_now = photo_error(st);
-        constexpr int B = 32;
         double v = 0.0;
-        for (int k0 = a.n_items; k0 < (int)gridDim.x; k0 += B) {
-            double pv[B];
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                pv[u] = k0 + u < (int)gridDim.x ? ld_sc1(a.item_out + 48 * (size_t)(k0 + u) + w) : 0.0;
-#pragma unroll
-            for (int u = 0; u < B; ++u)
-                if (k0 + u < (int)gridDim.x) v += pv[u];
-        }
-        if (a.rank == 0) v += cn;
+        for (int k = a.n_items; k < (int)gridDim.x; ++k) v += itm[48 * k + w];   // chunk order
+        if (a.rank == 0) v += w ? cn1 : cn0;
         if (iter <= 0) v = 0.0;
         v = photo_flag_norm(err_now, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
     }
-    for (int t = tid; t < a.nblk * 48; t += blockDim.x) {
+    for (int t = tid; t < a.nblk * 48; t += kSchurThreads) {
         const int blk = t / 48, e = t % 48;
-        const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
+        const int k0 = sbi[blk], nk = sbi[blk + 1] - k0;
         int b1 = 0;
         while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
         const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
         if (e >= 36 && b1 != b2) continue;   // off-diagonal blocks: 36 entries, no r / JTE
-        double pv[kMaxItemsPerBlock];
-#pragma unroll
-        for (int q = 0; q < kMaxItemsPerBlock; ++q) pv[q] = q < nk ? ld_sc1(a.item_out + 48 * (size_t)(k0 + q) + e) : 0.0;
         double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < kMaxItemsPerBlock; ++q) v += q < nk ? pv[q] : 0.0;
+        for (int q = 0; q < nk; ++q) v += itm[48 * (k0 + q) + e];   // item order (level 1's sums)
         if (e < 36) {
             const int ii = e / 6, jj = e % 6, i = 6 * b1 + ii, j = 6 * b2 + jj;
             if (b1 != b2 || ii <= jj) {
@@ -3428,7 +3445,7 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
 #ifndef MCC_SCHUR_LOADS
 #define MCC_SCHUR_LOADS 32
 #endif
-__global__ __launch_bounds__(256) void k_schur(SchurArgs a) {
+__global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
     // the warm solve's copy of this step's [S | r] (m > 30): prev2[iteration & 1] (same cache line as done)
@@ -4012,8 +4029,8 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, siz
 hipError_t mcc_launch_schur(const SchurArgs& a, int grid, hipStream_t s) {
     // LDS for the solve only when this launch solves (single GPU, m <= 30): the item workgroups
     // keep their occupancy
-    const size_t shm = a.fuse_solve ? (size_t)(a.m * a.m + a.m + (a.ssinv ? a.m * a.m : 0)) * sizeof(double) : 0;
-    hipLaunchKernelGGL(k_schur, dim3(grid), dim3(256), shm, s, a);
+    const size_t shm = schur_lds_bytes(a.m, a.fuse_solve, a.ssinv != nullptr, a.one_level, grid, a.nblk);
+    hipLaunchKernelGGL(k_schur, dim3(grid), dim3(kSchurThreads), shm, s, a);
     return hipGetLastError();
 }
 hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {

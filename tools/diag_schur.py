@@ -45,6 +45,11 @@ for rep in range(3):
     gend = ph[:, 10][ph[:, 10] > 0]
     print(f"rep {rep}: k_group {len(g0)} groups: start spread {q(g0.max() - t0)}, end median {q(np.median(gend) - t0)}, last {q(gend.max() - t0)}"
           + (" (us)" if RT else " (ticks)"))
+    ok = (ph[:, 0] > 0) & (ph[:, 10] > 0)
+    if ok.any():   # k_group's phases (slots 1..10 from the group's own start), median over groups
+        rel = ph[ok][:, 1:11] - ph[ok][:, :1]
+        print("  k_group phases (median from group start): " + " ".join(
+            f"{k}:{q(np.median(rel[:, k - 1]))}" for k in range(1, 11) if (rel[:, k - 1] > 0).any()))
     fin = sch[sch[:, 7] > 0]
     items = sch[sch[:, 7] == 0]
     if len(items):

@@ -2,9 +2,10 @@
 """Per-phase shader-clock stamps of k_solve's m > 30 warm solve (MCC_DIAG build: make diag ->
 libmcc_diag.so, run with MCC_LIB=multi_camera_calibration_amd/libmcc_diag.so).  Median over
 repetitions of the last step's k_solve row:
-  0 entry | 4 state + packed loads + epochs checked (barrier) | 8 [S | r] staged in LDS, sprev stores
-  issued | 9 S_t^-1 loaded into LDS, rows of S gathered | 10 refined | 11 (direct elimination if any)
-  | 12 sprev drained | 5 after the solve | 6 camera update written
+  0 entry | 4 state + packed loads + epochs checked (barrier) | 8 [S | r] staged in LDS (epoch
+  published here when there is no inverse to use) | 9 S_t^-1 loaded into LDS, rows of S gathered
+  (epoch published) | 10 refined | 11 after the direct elimination, if any | 5 after the solve |
+  6 camera update written
     python tools/diag_solve.py [config3] [reps]"""
 import os
 import sys
@@ -30,14 +31,11 @@ for r in range(reps):
     st = ba.stamps()
     rows.append(st)
 ba.close()
-# k_solve's row is the last 16 entries of the stamp buffer (mcc_debug_stamps' layout), and stamp 12
-# (sprev drained) the highest index the warm path writes
-st = rows[-1]
-last = int(np.nonzero(st)[0].max())
-base = last - 12   # stamp 12 is the highest index k_solve writes
-labels = {0: "entry", 4: "loads+epochs", 8: "staged+sprev issued", 9: "Sinv in LDS", 10: "refined", 11: "after GJ",
-          12: "sprev drained", 5: "solved", 6: "update"}
-order = [0, 4, 8, 9, 10, 11, 12, 5, 6]
+# k_solve's row is the last 16 entries of the stamp buffer (mcc_debug_stamps' layout)
+base = len(rows[-1]) - 16
+labels = {0: "entry", 4: "loads+epochs", 8: "staged", 9: "Sinv in LDS", 10: "refined", 11: "after GJ",
+          5: "solved", 6: "update"}
+order = [0, 4, 8, 9, 10, 11, 5, 6]
 vals = np.array([[r[base + k] for k in order] for r in rows], dtype=np.int64)
 d = np.diff(vals, axis=1)
 med = np.median(d, axis=0)
