@@ -184,12 +184,6 @@ struct mcc_problem {
     int poison_level = 0;
     bool peer_push = true;   // m > 30 with the peer transport: k_peer_push sends from many workgroups
     int schur_one_level = 0; // k_schur's single hand-off level (m <= 30; MCC_SCHUR_ONE_LEVEL=0 restores two)
-    // k_group's own hand-off (m <= 30, no k_schur launch; MCC_GROUP_TAIL=0 restores k_schur): clusters
-    // of tail_kc consecutive groups, cluster tickets, then one final ticket (group_tail, mcc_kernels.hip)
-    int group_tail = 0, tail_kc = 1, tail_ncl = 0;
-    DevBuf<int> tail_cnt;
-    DevBuf<int2> tail_run;
-    DevBuf<double> tail_out, tail_norm;
     int n_prep = 0, prep_lanes = 1;   // MCC_PREP_LANES=4: k_prep4 (measured slower at configs 3 and 5)
     // warm solve (m > 30 split step, MCC_WARM=0 turns it off): a resident helper kernel on a side
     // stream (one per batch of update steps) inverts each step's reduced system while the next step
@@ -291,7 +285,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     if (p->poison) {
         // (with the warm solve the packed system carries the previous step's system into the next
         // step, like dg: it is an input of the step, not a hand-off inside it, and stays unpoisoned)
-        for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed, &p->ssinv, &p->tail_out, &p->tail_norm})
+        for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed, &p->ssinv})
             if (b->p && b->n && !(swarm && b == &p->packed))
                 HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
         if (swarm) HIPCHK(hipMemsetAsync(p->ssinv_ok.p, 0xFF, sizeof(int), p->stream));
@@ -330,10 +324,6 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.fault_photo = p->fault_photo;
     la.ssinv = swarm ? p->ssinv.p : nullptr;
     la.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
-    const bool tail = p->group_tail && p->use_group && !p->fused;
-    la.tail = tail ? 1 : 0;
-    la.tail_kc = p->tail_kc; la.tail_ncl = p->tail_ncl;
-    la.tail_cnt = p->tail_cnt.p; la.tail_run = p->tail_run.p; la.tail_out = p->tail_out.p; la.tail_norm = p->tail_norm.p;
     // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
     // split path: the packed system is summed by RCCL and solved by k_solve.  The peer transport
     // keeps one kernel per step: the final arriver exchanges with the peers and solves.
@@ -342,7 +332,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
     la.fused = p->fused;
     la.group_size = p->group_size; la.n_groups = p->n_groups;
     la.rank = p->rank; la.fuse_solve = rccl ? 0 : 1;
-    la.peer = peer_ctx(p, peer && (p->fused || tail));
+    la.peer = peer_ctx(p, peer && p->fused);
     la.contrib = p->contrib.p; la.gsum = p->gsum.p; la.cnt = p->cnt.p; la.packed = p->packed.p; la.W = p->W.p;
     la.solve = solve_ctx(p, do_update);
     la.solve.stamps = nullptr;
@@ -357,7 +347,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
             HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     }
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
-    if (p->fused || tail) {   // the linearisation kernel's final arriver summed the system
+    if (p->fused) {
         if (rccl) {
             const bool tx = tim && p->ev_x_used + 2 <= (int)p->ev_x.size();
             if (tx) HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used], p->stream));
@@ -815,36 +805,6 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // MCC_ENOTPD (the device positive-definiteness check of the solve).
     p->n_items = (int)items.size();
     p->n_pairs = n_slots;
-    // k_group's own hand-off: clusters of ~sqrt(groups) consecutive groups (<= kTailMaxKC each, <=
-    // kTailMaxCl of them), a run of slots per (cluster, block) -- a block's slots are in group order
-    std::vector<int2> tail_run;
-    {
-        const bool ok = p->use_group && !p->fused && p->m <= 30 && NG >= 1 && NG <= mcc::kTailMaxKC * mcc::kTailMaxCl;
-        p->group_tail = ok ? 1 : 0;
-        if (const char* f = std::getenv("MCC_GROUP_TAIL")) p->group_tail = ok && std::atoi(f) != 0;
-        if (p->group_tail) {
-            int kc = (int)std::ceil(std::sqrt((double)NG));
-            kc = std::max(kc, (NG + mcc::kTailMaxCl - 1) / mcc::kTailMaxCl);
-            kc = std::min(kc, mcc::kTailMaxKC);
-            p->tail_kc = kc;
-            p->tail_ncl = (NG + kc - 1) / kc;
-            std::vector<int> grp_of(gpairs.size());
-            for (int g = 0; g < NG; ++g)
-                for (int q = gpair_ptr[g]; q < gpair_ptr[g + 1]; ++q) grp_of[q] = g;
-            tail_run.assign((size_t)p->tail_ncl * p->nblk, make_int2(0, 0));
-            for (int b = 0; b < p->nblk; ++b) {
-                int b1 = 0;
-                while (b1 + 1 < nb && blk_index(b1 + 1, b1 + 1) <= b) ++b1;
-                const int dflag = blk_index(b1, b1) == b ? 1 << 16 : 0;
-                for (int c = 0; c < p->tail_ncl; ++c) tail_run[(size_t)c * p->nblk + b].y = dflag;
-                for (int src : blk_src[b]) {
-                    int2& r = tail_run[(size_t)(grp_of[src] / kc) * p->nblk + b];
-                    if ((r.y & 0xffff) == 0) r.x = gpairs[src].w;
-                    ++r.y;
-                }
-            }
-        }
-    }
     p->n_norm_chunks = (V + 255) / 256;
     // one hand-off level (m <= 30) while the final arriver loads everything in one batch
     const bool one_fits = p->m <= 30 && 48 * (p->n_items + p->n_norm_chunks) + p->m * p->m <= mcc::kSchurOneLevelLoads * 256;
@@ -949,16 +909,6 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     HIPC(hipMemset(p->counter.p, 0, sizeof(int)));
     HIPC(p->cnt_blk.alloc(p->nblk));
     HIPC(hipMemset(p->cnt_blk.p, 0, sizeof(int) * std::max(p->nblk, 1)));
-    if (p->group_tail) {
-        HIPC(p->tail_run.upload(tail_run.data(), tail_run.size()));
-        HIPC(p->tail_out.alloc((size_t)p->tail_ncl * p->nblk * 48));
-        HIPC(hipMemset(p->tail_out.p, 0, sizeof(double) * p->tail_out.n));
-        HIPC(p->tail_norm.alloc(2 * (size_t)p->tail_ncl));
-        HIPC(p->tail_cnt.alloc(p->tail_ncl + 1));
-        HIPC(hipMemset(p->tail_cnt.p, 0, sizeof(int) * (p->tail_ncl + 1)));
-        // the final arriver's S and r, and a cluster's photo norm partials, in k_group's LDS
-        p->group_shmem = std::max(p->group_shmem, std::max((size_t)(p->m * p->m + p->m), (size_t)256) * sizeof(double));
-    }
     p->ntri = p->m * (p->m + 1) / 2;
     p->packed_len = p->ntri + 2 * p->m + 2;
     HIPC(p->packed.alloc(p->packed_len));
@@ -993,7 +943,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // refinement (~3 us on one wave, reading S and the inverse from LDS) and the inverse's loads cost
     // more than the register Gauss-Jordan they replace (config4, interleaved: 30.0 vs 29.5 us per step)
     {
-        bool sw = !p->fused && p->use_group && p->schur_one_level && !p->group_tail &&
+        bool sw = !p->fused && p->use_group && p->schur_one_level &&
                   p->group_shmem >= (size_t)2 * p->m * p->m * sizeof(double);   // the spare's [S | I] in LDS
         const char* f = std::getenv("MCC_SMALL_WARM");
         sw = sw && f && std::atoi(f) != 0;
@@ -1062,7 +1012,6 @@ void mcc_destroy(mcc_problem* p) {
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
-    p->tail_cnt.release(); p->tail_run.release(); p->tail_out.release(); p->tail_norm.release();
     p->edge_photo.release(); p->edge_info.release(); p->items.release(); p->gpairs.release();
     p->prep_ptr.release(); p->prep_edge.release();
     p->pgrp_ptr.release(); p->pgrp_edge.release(); p->edge_lphoto.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();

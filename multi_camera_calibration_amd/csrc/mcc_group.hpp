@@ -511,13 +511,8 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
                 g2 += xs[8 + q] * xs[8 + q];
                 x2 += xs[q] * xs[q];
             }
-            if (a.tail) {
-                st_sc1(a.photo_norm + 2 * (size_t)(p0 + pq), g2);
-                st_sc1(a.photo_norm + 2 * (size_t)(p0 + pq) + 1, x2);
-            } else {
-                a.photo_norm[2 * (size_t)(p0 + pq)] = g2;
-                a.photo_norm[2 * (size_t)(p0 + pq) + 1] = x2;
-            }
+            a.photo_norm[2 * (size_t)(p0 + pq)] = g2;
+            a.photo_norm[2 * (size_t)(p0 + pq) + 1] = x2;
         }
         const double om1[3] = {xs[0], xs[1], xs[2]};
         Rot r1;
@@ -804,20 +799,11 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
         }
         if (h == 0) {
             double* out = a.pairprod + (size_t)pqv.w;
-            if (a.tail) {   // write-through: the cluster's last arriver reads them (group_tail)
 #pragma unroll
-                for (int j = 0; j < 6; ++j) st_sc1(out + i0 * 6 + j, acc[j]);
-                if (diag) {
-                    st_sc1(out + 36 + i0, racc);
-                    st_sc1(out + 42 + i0, jacc);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 6; ++j) out[i0 * 6 + j] = acc[j];
-                if (diag) {
-                    out[36 + i0] = racc;
-                    out[42 + i0] = jacc;
-                }
+            for (int j = 0; j < 6; ++j) out[i0 * 6 + j] = acc[j];
+            if (diag) {
+                out[36 + i0] = racc;
+                out[42 + i0] = jacc;
             }
         }
     }
@@ -826,7 +812,6 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     __syncthreads();
     SSTAMP(stp, 10, 0);
 #endif
-    if (a.tail) group_tail<NT>(a, grp, smem);
 }
 
 // ---------------------------------------------------------------- k_prep4

@@ -115,15 +115,7 @@ struct LinArgs {
     // m <= 30 warm solve: k_group's spare workgroup inverts the previous step's packed system
     double* ssinv;           // [m x m] (null: off)
     int* ssinv_ok;           // 1: ssinv holds the previous update step's inverse
-    // k_group's own hand-off (m <= 30, group_tail in mcc_kernels.hip; no k_schur launch)
-    int tail, tail_kc, tail_ncl;   // on; groups per cluster; clusters
-    int* tail_cnt;           // [tail_ncl + 1] tickets (cluster, final), zero between launches
-    const int2* tail_run;    // [tail_ncl x nblk] {first slot's offset, slot count | diagonal << 16}
-    double* tail_out;        // [tail_ncl x nblk x 48] cluster sums of the blocks
-    double* tail_norm;       // [tail_ncl x 2] cluster sums of the photo norm partials
 };
-constexpr int kTailMaxKC = 16;   // groups per cluster, at most (a cluster's sums: one batch of loads)
-constexpr int kTailMaxCl = 16;   // clusters, at most (the final sums: one batch): <= 256 groups
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
 constexpr int kPhotoGroup = 8;        // photos per k_photo workgroup, at most

@@ -3853,151 +3853,6 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
     }
 }
 
-// ---------------------------------------------------------------- k_group's own hand-off (m <= 30)
-// With the group tail (LinArgs::tail) k_group also does k_schur's work, without k_schur's launch:
-// every group writes its slots and its photos' norm partials write-through (sc1) and takes a ticket
-// of its cluster (tail_kc consecutive groups); the cluster's last arriver sums each camera-pair
-// block's slots of its groups in group order, and its photos' norm partials in photo order, into
-// tail_out / tail_norm and takes the final ticket; the last cluster sums the clusters in cluster
-// order into the packed system and solves (single GPU, peer transport) or leaves it for the
-// all-reduce and k_solve.  Both levels load everything they sum in one batch of unconditional
-// loads.  On config4 this removes the k_group -> k_schur kernel boundary and k_schur's item round
-// from the step's tail.
-template <int NT>
-__device__ __forceinline__ void group_tail(const LinArgs& a, int grp, double* sm) {
-    State* st = a.state;
-    const int tid = threadIdx.x;
-    const int m = a.global_dim, nb = m / 6, nblk = nb * (nb + 1) / 2, ntri = m * (m + 1) / 2, nent = 48 * nblk;
-    constexpr int E = (15 * 48 + NT - 1) / NT;   // entries per thread (nblk <= 15 at m <= 30)
-    const int kc = a.tail_kc, ncl = a.tail_ncl;
-    const int cl = grp / kc, g0 = cl * kc, g1 = min(g0 + kc, a.n_pgroups);
-    // the cluster's runs {first slot's offset, slot count | diagonal << 16} (host data) and photo
-    // range, loaded ahead of the ticket
-    int2 run[E];
-#pragma unroll
-    for (int u = 0; u < E; ++u) {
-        const int t = tid + u * NT;
-        run[u] = a.tail_run[(size_t)cl * nblk + (t < nent ? t / 48 : 0)];
-    }
-    const int ph0 = a.pgrp_ptr[g0], ph1 = a.pgrp_ptr[g1];
-    if (!arrive_last_sc1(a.tail_cnt + cl, g1 - g0)) return;
-
-    // ---- cluster level: one batch (the photo norms, then E entries x kTailMaxKC slots per thread)
-    {
-        const int npn = 2 * (ph1 - ph0);   // <= 2 kTailMaxKC kPhotoGroup <= NT
-        const double pn = ld_sc1(a.photo_norm + 2 * (size_t)ph0 + (tid < npn ? tid : 0));
-        double v[E][kTailMaxKC];
-#pragma unroll
-        for (int u = 0; u < E; ++u) {
-            const int t = tid + u * NT, e = t % 48;
-            const int off = run[u].x, cnt = run[u].y & 0xffff;
-            const bool diag = (run[u].y >> 16) != 0;
-            const int stride = diag ? 48 : 36, ee = diag ? e : min(e, 35);
-#pragma unroll
-            for (int q = 0; q < kTailMaxKC; ++q) {
-                const int qq = q < cnt ? q : (cnt > 0 ? cnt - 1 : 0);
-                v[u][q] = ld_sc1(a.pairprod + (size_t)off + (size_t)qq * stride + ee);
-            }
-        }
-        if (tid < npn) sm[tid] = pn;
-#pragma unroll
-        for (int u = 0; u < E; ++u) {
-            const int t = tid + u * NT, e = t % 48;
-            const int cnt = run[u].y & 0xffff;
-            const bool diag = (run[u].y >> 16) != 0;
-            double s = 0.0;
-#pragma unroll
-            for (int q = 0; q < kTailMaxKC; ++q)
-                if (q < cnt) s += v[u][q];
-            if (t < nent && (e < 36 || diag)) st_sc1(a.tail_out + (size_t)cl * nent + t, s);
-        }
-        __syncthreads();
-        if (tid < 2) {
-            double s = 0.0;
-            for (int q = tid; q < npn; q += 2) s += sm[q];   // photo order
-            st_sc1(a.tail_norm + 2 * cl + tid, s);
-        }
-    }
-    if (!arrive_last_sc1(a.tail_cnt + ncl, ncl)) return;
-
-    // ---- final level: the clusters in order (one batch: state words, norms, E entries x ncl)
-    const int iter = st->iter;
-    const double cn0 = st->cam_normG2, cn1 = st->cam_normX2;
-    const int err_now = photo_error(st);
-    double w[E][kTailMaxCl], nv[kTailMaxCl];
-#pragma unroll
-    for (int q = 0; q < kTailMaxCl; ++q) nv[q] = ld_sc1(a.tail_norm + 2 * (q < ncl ? q : ncl - 1) + (tid & 1));
-#pragma unroll
-    for (int u = 0; u < E; ++u) {
-        const int t = tid + u * NT, tt = t < nent ? t : 0;
-#pragma unroll
-        for (int q = 0; q < kTailMaxCl; ++q) w[u][q] = ld_sc1(a.tail_out + (size_t)(q < ncl ? q : ncl - 1) * nent + tt);
-    }
-    double* S = sm;          // m*m
-    double* r = sm + m * m;  // m
-    __shared__ double norms[2];
-    const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
-    if (tid < 2) {
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < kTailMaxCl; ++q)
-            if (q < ncl) v += nv[q];
-        if (a.rank == 0) v += tid ? cn1 : cn0;
-        if (iter <= 0) v = 0.0;
-        v = photo_flag_norm(err_now, tid, v);
-        norms[tid] = v;
-        a.packed[ntri + 2 * m + tid] = v;
-    }
-#pragma unroll
-    for (int u = 0; u < E; ++u) {
-        const int t = tid + u * NT;
-        if (t >= nent) continue;
-        const int blk = t / 48, e = t % 48;
-        int b1 = 0;
-        while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
-        const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
-        if (e >= 36 && b1 != b2) continue;   // off-diagonal blocks: 36 entries, no r / JTE
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < kTailMaxCl; ++q)
-            if (q < ncl) v += w[u][q];
-        if (e < 36) {
-            const int ii = e / 6, jj = e % 6, i = 6 * b1 + ii, j = 6 * b2 + jj;
-            if (b1 != b2 || ii <= jj) {
-                a.packed[packed_index(i, j, m)] = v;
-                if (lds) {
-                    S[i * m + j] = v;
-                    S[j * m + i] = v;
-                }
-            }
-        } else {
-            const int wv = (e - 36) / 6, i = 6 * b1 + (e - 36) % 6;
-            a.packed[ntri + wv * m + i] = v;   // r (wv = 0), JTE of the global block (wv = 1)
-            if (lds && wv == 0) r[i] = v;
-        }
-    }
-    if (!a.fuse_solve) return;
-    __syncthreads();
-    if (a.peer.nranks > 0) {
-        // multi-GPU: the rank-ordered sum of every rank's system, then this rank solves it
-        if (!peer_exchange(a.peer, st, a.packed)) return;
-        for (int t = tid; t < ntri + m; t += NT) {
-            const double v = a.packed[t];
-            if (t < ntri) {
-                int i, j;
-                packed_ij(t, m, i, j);
-                S[i * m + j] = v;
-                S[j * m + i] = v;
-            } else {
-                r[t - ntri] = v;
-            }
-        }
-        if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
-        __syncthreads();
-    }
-    solve_global<false>(a.solve, S, r, norms[0], norms[1], nullptr, nullptr);
-}
-
 #include "mcc_group.hpp"
 
 }  // namespace mcc

@@ -77,9 +77,6 @@ CASES["config3_small_split3"] = CASES["config3_small"]
 for _n in ["config4_small", "pinhole_back", "omni_skew"]:
     CASES[_n + "_g16"] = CASES[_n]
 CASES["config3_small_g32"] = CASES["config3_small"]
-# k_group -> k_schur (MCC_GROUP_TAIL=0) where k_group otherwise hands off by itself (group_tail)
-for _n in ["config4_small", "pinhole_back", "config2_small"]:
-    CASES[_n + "_tail0"] = CASES[_n]
 # the three-kernel step's k_prep4 (4 lanes per edge prologue, MCC_PREP_LANES=4; default k_prep, one lane)
 for _n in ["config3_small", "pinhole_back", "config5_small"]:
     CASES[_n + "_prep4"] = CASES[_n]
@@ -97,8 +94,6 @@ def make_adjuster(name, p):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "16"}
     elif name.endswith("_g32"):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "32"}
-    elif name.endswith("_tail0"):
-        env = {"MCC_FUSED": "0", "MCC_GROUP_TAIL": "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -120,8 +115,7 @@ def case(request):
 def test_forced_step_kernels(case):
     """The A/B suffixes reach the linearisation kernels they name (mcc_problem_path)."""
     name, p, o, g = case
-    want = {"_split3": "k_prep+k_edge+k_photo", "_prep4": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group",
-            "_tail0": "k_group"}
+    want = {"_split3": "k_prep+k_edge+k_photo", "_prep4": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group"}
     for suf, k in want.items():
         if name.endswith(suf):
             assert g.step_kernels() == k, name

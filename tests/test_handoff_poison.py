@@ -52,8 +52,7 @@ def run(p, poison, env, steps):   # poison: 0 off, 1 the hand-off buffers, 2 als
 
 @pytest.mark.parametrize("cfg,env,want", [
     ("config2", {}, "k_linearize"),                    # fused: 500 photos, 2 per CU, two ticket levels
-    ("config4", {}, "k_group"),                        # k_group's own hand-off (clusters, final, solve)
-    ("config4", {"MCC_GROUP_TAIL": "0"}, "k_group"),   # k_group -> k_schur (items, one level, solve)
+    ("config4", {}, "k_group"),                        # k_group -> k_schur (items, blocks, solve)
     ("config5", {}, "k_prep+k_edge+k_photo"),          # three-kernel split step, DoubleSide m = 6
     ("config3", {}, "k_prep+k_edge+k_photo"),          # m = 90: k_schur -> k_solve
     ("config5", {"MCC_GROUP": "1"}, "k_group"),        # k_group at 999 groups (4 per CU)

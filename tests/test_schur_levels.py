@@ -41,8 +41,8 @@ def _run(p, env):
 
 
 @pytest.mark.parametrize("cfg,env,want", [
-    ("config4", {"MCC_GROUP_TAIL": "0"}, "k_group"),                     # the headline on k_group -> k_schur
-    ("config2", {"MCC_FUSED": "0", "MCC_GROUP_TAIL": "0"}, "k_group"),   # pinhole m = 18 on the split step
+    ("config4", {}, "k_group"),                                          # the headline: k_group -> k_schur
+    ("config2", {"MCC_FUSED": "0"}, "k_group"),                           # pinhole m = 18 on the split step
     ("config5", {}, "k_prep+k_edge+k_photo"),                             # DoubleSide m = 6, three kernels
 ])
 def test_one_level_is_bitwise_two_level(cfg, env, want):
@@ -53,21 +53,3 @@ def test_one_level_is_bitwise_two_level(cfg, env, want):
     assert a[3] == b[3]
     for u, v in zip(a[:5], b[:5]):
         assert np.array_equal(np.asarray(u), np.asarray(v))
-
-
-@pytest.mark.parametrize("cfg,env", [
-    ("config4", {}),                       # the headline: 250 groups, 16 clusters of 16
-    ("config2", {"MCC_FUSED": "0"}),       # 125 groups, 11 clusters of 12
-])
-def test_group_tail_matches_k_schur(cfg, env):
-    """k_group's own hand-off (group_tail: clusters of consecutive groups, then the clusters; no k_schur
-    launch) sums the same slots in another order than k_schur's items: the results agree to rounding
-    (1e-9 of the largest entry), and the optimize loop takes the same number of iterations."""
-    p = rig.make_config(cfg)
-    a = _run(p, dict(env, MCC_GROUP_TAIL="1"))
-    b = _run(p, dict(env, MCC_GROUP_TAIL="0"))
-    assert a[5] == b[5] == "k_group"
-    assert a[3] == b[3]
-    for u, v in zip(a[:5], b[:5]):
-        u, v = np.asarray(u, np.float64), np.asarray(v, np.float64)
-        assert np.abs(u - v).max() <= 1e-9 * max(np.abs(v).max(), 1e-300), (cfg, np.abs(u - v).max())
