@@ -409,7 +409,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
         SolveArgs so{solve_ctx(p, do_update), p->packed.p, peer_ctx(p, peer), 0, {}};
         // MCC_DIAG: k_solve's phase stamps after k_schur's rows
         so.ctx.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) +
-                                          8 * (size_t)(p->n_items + p->n_norm_chunks)
+                                          mcc::kSchurStampStride * (size_t)(p->n_items + p->n_norm_chunks)
                                     : nullptr;
         if (p->warm && do_update) so.warm = warm_ctx(p);
         if (peer && p->peer_push) {   // MCC_PEER_PUSH=0: k_solve's one workgroup sends too
@@ -1246,7 +1246,7 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     if (!p->stamps.p) {
-        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + 8 * (size_t)(p->n_items + p->n_norm_chunks) + 16;
+        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + mcc::kSchurStampStride * (size_t)(p->n_items + p->n_norm_chunks) + 16;
         HIPCHK(p->stamps.alloc(n_st));
         HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
         for (auto& g : p->gexec)

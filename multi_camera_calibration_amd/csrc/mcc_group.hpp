@@ -633,6 +633,13 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
         wave_sync_lds();   // this wave's chain records are consumed before the next round's corners
         if (rb == 0) SSTAMP(stp, 5, 0);
     }
+#ifdef MCC_DIAG
+    if (stp && lane == 0 && wave < 16) {   // per wave: the rounds done (slots 16 + wave)
+        __builtin_amdgcn_sched_barrier(0);
+        stp[16 + wave] = (long long)MCC_DIAG_CLOCK();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
     __syncthreads();
     SSTAMP(stp, 6, 0);
 

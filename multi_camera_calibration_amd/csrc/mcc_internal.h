@@ -8,6 +8,7 @@
 namespace mcc {
 
 constexpr int kStampStride = 32;   // MCC_DIAG: s_memtime / s_memrealtime slots per k_linearize workgroup
+constexpr int kSchurStampStride = 16;   // MCC_DIAG: slots per k_schur workgroup (after k_linearize's rows)
 
 // Device-resident loop state of optimizeExtrinsics (src/multicalib.cpp:468-507).
 struct State {

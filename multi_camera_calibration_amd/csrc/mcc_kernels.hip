@@ -3342,7 +3342,7 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     State* st = a.state;
     const int tid = threadIdx.x;
     if (!arrive_last_sc1(a.counter, (int)gridDim.x)) return;
-    STAMPP(a.stamps, 8, 2);
+    STAMPP(a.stamps, kSchurStampStride, 2);
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;          // m*m
@@ -3362,46 +3362,75 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     const int err_now = photo_error(st);
     const int ivok = Iv ? a.ssinv_ok[0] : 0;
     {
-        // one batch, no loop (a loop's header waits for the previous iteration's loads, and so for
-        // the state loads above): the host keeps 48 grid + m^2 <= kSchurOneLevelLoads * 256
+        // one batch of U loads per thread, no loop (a loop's header waits for the previous iteration's
+        // loads, and so for the state loads above), U the smallest of 4 / 8 / 16 that covers n: a
+        // lane past n re-reads element n - 1, and rows of such loads -- many requests for one
+        // address -- cost ~1.5 us at config4 when U was 16 for n = 912.  The host keeps 48 grid + m^2
+        // <= kSchurOneLevelLoads * 256.
         const int nI = 48 * (int)gridDim.x, nV = Iv ? m * m : 0, n = nI + nV;
-        constexpr int U = kSchurOneLevelLoads;
-        double v[U];
+        auto batch = [&](auto UC) {
+            constexpr int U = decltype(UC)::value;
+            double v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            int t = u * kSchurThreads + tid;
-            t = t < n ? t : n - 1;
-            v[u] = ld_sc1(t < nI ? a.item_out + t : a.ssinv + (t - nI));
-        }
+            for (int u = 0; u < U; ++u) {
+                int t = u * kSchurThreads + tid;
+                t = t < n ? t : n - 1;
+                v[u] = ld_sc1(t < nI ? a.item_out + t : a.ssinv + (t - nI));
+            }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int t = u * kSchurThreads + tid;
-            if (t < nI) itm[t] = v[u];
-            else if (t < n) Iv[t - nI] = v[u];
-        }
+            for (int u = 0; u < U; ++u) {
+                const int t = u * kSchurThreads + tid;
+                if (t < nI) itm[t] = v[u];
+                else if (t < n) Iv[t - nI] = v[u];
+            }
+        };
+        static_assert(kSchurOneLevelLoads == 16, "k_schur one-level batch sizes");
+        if (n <= 4 * kSchurThreads) batch(std::integral_constant<int, 4>{});
+        else if (n <= 8 * kSchurThreads) batch(std::integral_constant<int, 8>{});
+        else batch(std::integral_constant<int, 16>{});
     }
     if (tid <= a.nblk) sbi[tid] = bi;
     if (tid == 0) iv_ok = ivok;
     __syncthreads();
+    STAMPP(a.stamps, kSchurStampStride, 8);   // the batch landed in LDS
+    // the sums first, every global store after them: a loop entered with a store in flight gets
+    // an s_waitcnt vmcnt(0) at its head (the compiler's pre-loop flush), which waits for the store's
+    // completion -- 1.5 us at config4 when the packed stores sat between the sums' loops
+    constexpr int EU = (15 * 48 + kSchurThreads - 1) / kSchurThreads;   // entries per thread (m <= 30)
+    const int nent = a.nblk * 48;
+    double ev[EU];
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+        const int t = tid + u * kSchurThreads;
+        double v = 0.0;
+        if (t < nent) {
+            const int blk = t / 48, e = t % 48;
+            const int k0 = sbi[blk], nk = sbi[blk + 1] - k0;
+            for (int q = 0; q < nk; ++q) v += itm[48 * (k0 + q) + e];   // item order (level 1's sums)
+        }
+        ev[u] = v;
+    }
+    double nrm = 0.0;
     if (tid < 2) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
-        double v = 0.0;
-        for (int k = a.n_items; k < (int)gridDim.x; ++k) v += itm[48 * k + w];   // chunk order
-        if (a.rank == 0) v += w ? cn1 : cn0;
-        if (iter <= 0) v = 0.0;
-        v = photo_flag_norm(err_now, w, v);
-        norms[w] = v;
-        a.packed[ntri + 2 * m + w] = v;
+        for (int k = a.n_items; k < (int)gridDim.x; ++k) nrm += itm[48 * k + w];   // chunk order
+        if (a.rank == 0) nrm += w ? cn1 : cn0;
+        if (iter <= 0) nrm = 0.0;
+        nrm = photo_flag_norm(err_now, w, nrm);
+        norms[w] = nrm;
     }
-    for (int t = tid; t < a.nblk * 48; t += kSchurThreads) {
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+        const int t = tid + u * kSchurThreads;
+        if (t >= nent) continue;
         const int blk = t / 48, e = t % 48;
-        const int k0 = sbi[blk], nk = sbi[blk + 1] - k0;
-        int b1 = 0;
-        while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
+        int b1 = 0;   // the block's row: the last b with first_block(b) <= blk (nb <= 5)
+#pragma unroll
+        for (int b = 1; b < 5; ++b)
+            if (b < nb && b * nb - b * (b - 1) / 2 <= blk) b1 = b;
         const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
         if (e >= 36 && b1 != b2) continue;   // off-diagonal blocks: 36 entries, no r / JTE
-        double v = 0.0;
-        for (int q = 0; q < nk; ++q) v += itm[48 * (k0 + q) + e];   // item order (level 1's sums)
+        const double v = ev[u];
         if (e < 36) {
             const int ii = e / 6, jj = e % 6, i = 6 * b1 + ii, j = 6 * b2 + jj;
             if (b1 != b2 || ii <= jj) {
@@ -3417,6 +3446,8 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
             if (lds && w == 0) r[i] = v;
         }
     }
+    if (tid < 2) a.packed[ntri + 2 * m + tid] = nrm;
+    STAMPP(a.stamps, kSchurStampStride, 9);   // sums placed (thread 0)
     if (!a.fuse_solve) return;
     __syncthreads();   // the packed system and the norms (this workgroup's global stores and LDS)
     if (a.peer.nranks > 0) {
@@ -3436,11 +3467,11 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
         if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
         __syncthreads();
     }
-    STAMPP(a.stamps, 8, 3);
+    STAMPP(a.stamps, kSchurStampStride, 3);
     SolveCtx sc = a.solve;
-    sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
+    sc.stamps = a.stamps ? a.stamps + kSchurStampStride * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
     solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, Iv && iv_ok ? Iv : nullptr);
-    STAMPP(a.stamps, 8, 7);
+    STAMPP(a.stamps, kSchurStampStride, 7);
 }
 #ifndef MCC_SCHUR_LOADS
 #define MCC_SCHUR_LOADS 32
@@ -3450,7 +3481,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     if (st->done) return;
     // the warm solve's copy of this step's [S | r] (m > 30): prev2[iteration & 1] (same cache line as done)
     double* prev = a.prev2 ? a.prev2 + (size_t)(st->iter & 1) * a.prev_stride : nullptr;
-    STAMPP(a.stamps, 8, 0);
+    STAMPP(a.stamps, kSchurStampStride, 0);
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
     __shared__ double part[kSub][48];
@@ -3501,7 +3532,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
             __syncthreads();
         }
     }
-    STAMPP(a.stamps, 8, 1);
+    STAMPP(a.stamps, kSchurStampStride, 1);
     if (a.one_level) {
         schur_one_level(a);
         return;
@@ -3524,7 +3555,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
             schur_block_store(a, blk, tid, v, prev);
         }
     }
-    STAMPP(a.stamps, 8, 2);
+    STAMPP(a.stamps, kSchurStampStride, 2);
     // ---- level 2: the last of the blocks and norm chunks adds the stop-test norms
     if (!arrive_last_sc1(a.counter, a.nblk + (int)gridDim.x - a.n_items)) return;
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -3563,7 +3594,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
         if (!peer_exchange(a.peer, st, a.packed)) return;
         if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
     }
-    STAMPP(a.stamps, 8, 3);
+    STAMPP(a.stamps, kSchurStampStride, 3);
     for (int t = tid; t < ntri + m; t += blockDim.x) {
         const double v = ld_sc1(a.packed + t);
         if (t < ntri) {
@@ -3577,9 +3608,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     }
     __syncthreads();
     SolveCtx sc = a.solve;
-    sc.stamps = a.stamps ? a.stamps + 8 * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
+    sc.stamps = a.stamps ? a.stamps + kSchurStampStride * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
     solve_global<false>(sc, S, r, norms[0], norms[1]);
-    STAMPP(a.stamps, 8, 7);
+    STAMPP(a.stamps, kSchurStampStride, 7);
 }
 
 // ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)

@@ -38,7 +38,7 @@ for rep in range(3):
     raw = ba.stamps().reshape(-1)
     nv = max(p.n_photos, 1)
     ph = raw[:32 * nv].reshape(nv, 32)
-    sch = raw[32 * nv:].reshape(-1, 8)
+    sch = raw[32 * nv:-16].reshape(-1, 16)
     sch = sch[(sch != 0).any(axis=1)]
     g0 = ph[:, 0][ph[:, 0] > 0]
     t0 = g0.min()
@@ -50,13 +50,18 @@ for rep in range(3):
         rel = ph[ok][:, 1:11] - ph[ok][:, :1]
         print("  k_group phases (median from group start): " + " ".join(
             f"{k}:{q(np.median(rel[:, k - 1]))}" for k in range(1, 11) if (rel[:, k - 1] > 0).any()))
-    fin = sch[sch[:, 7] > 0]
+    if ok.any():   # per wave: the edge rounds done (slots 16 + wave), median over groups
+        w = ph[ok][:, 16:24] - ph[ok][:, :1]
+        print("  k_group rounds done per wave (median from group start): " + " ".join(
+            f"w{k}:{q(np.median(w[:, k]))}" for k in range(8) if (w[:, k] > 0).all()))
+    fin = sch[sch[:, 7] > t0]   # (rows of earlier launches: stale final stamps, skipped)
     items = sch[sch[:, 7] == 0]
     if len(items):
         lv1 = items[:, 2][items[:, 2] > 0]
         print(f"  k_schur items: {len(items)}, start min {q(items[:, 0].min() - t0)} max {q(items[:, 0].max() - t0)}, "
               f"items summed max {q(items[:, 1].max() - t0)}, level-1 max {q(lv1.max() - t0) if len(lv1) else '-'}")
     for f in fin:
-        names = ["solve entry", "GJ start (w1)", "GJ end (w1)", "final: before packed loads", "stop-test barrier", "-", "camera update", "end"]
+        names = ["solve entry", "GJ start (w1)", "GJ end (w1)", "final: before packed loads", "stop-test barrier", "-",
+                 "camera update", "end", "one level: batch landed", "sums placed"]
         print("  final WG: " + ", ".join(f"{n} {q(v - t0)}" for n, v in zip(names, f) if v))
 ba.close()

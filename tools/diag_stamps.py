@@ -40,7 +40,7 @@ def main():
     raw = ba.stamps().reshape(-1)
     nv = max(p.n_photos, 1)
     s = raw[:32 * nv].reshape(nv, 32).astype(np.float64)
-    sch = raw[32 * nv:].reshape(-1, 8).astype(np.float64)
+    sch = raw[32 * nv:-16].reshape(-1, 16)[:, :8].astype(np.float64)
     s = s[s[:, 0] > 0]
     d = np.diff(s[:, :8], axis=1)
     print(f"{cfg}: {len(s)} workgroups stamped (s_memtime ticks)")
