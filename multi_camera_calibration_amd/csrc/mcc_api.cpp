@@ -939,14 +939,14 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         return bail(fail(MCC_EINVAL, "too many edges / Schur pairs of one photo group for k_group's LDS"));
     HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->use_group ? p->group_shmem : 0));
     // m <= 30 on k_group -> k_schur (config4): the previous system's inverse from a spare k_group
-    // workgroup, refinement in k_schur's final solve.  Opt-in (MCC_SMALL_WARM=1): at m = 18 the
-    // refinement (~3 us on one wave, reading S and the inverse from LDS) and the inverse's loads cost
-    // more than the register Gauss-Jordan they replace (config4, interleaved: 30.0 vs 29.5 us per step)
+    // workgroup, refinement in k_schur's final solve (MCC_SMALL_WARM=0: the register Gauss-Jordan
+    // only).  With S and the inverse in registers the refinement takes ~1.7 us at m = 18 against the
+    // elimination's ~2.6 (config4, interleaved: 28.9 vs 29.4 us per step); round 4's first form, reading
+    // them from LDS per product, took ~3 us and lost
     {
         bool sw = !p->fused && p->use_group && p->schur_one_level &&
                   p->group_shmem >= (size_t)2 * p->m * p->m * sizeof(double);   // the spare's [S | I] in LDS
-        const char* f = std::getenv("MCC_SMALL_WARM");
-        sw = sw && f && std::atoi(f) != 0;
+        if (const char* f = std::getenv("MCC_SMALL_WARM")) sw = sw && std::atoi(f) != 0;
         if (sw) {
             HIPC(p->ssinv.alloc((size_t)p->m * p->m));
             HIPC(p->ssinv_ok.alloc(1));

@@ -3138,44 +3138,61 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
     if (tid == 0) a.ssinv_ok[0] = ok ? 1 : 0;
 }
 
-// x = S^-1 r by refinement with Iv (LDS, m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
-// equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i (the warm solve's test), at
-// most kWarmMaxIters corrections, each cutting the error fourfold.  S, Iv and the vectors are read
-// from LDS as they are used (few registers: the solve's wave runs inside k_schur's final arriver).
-// On success r holds x.
-__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, double* xw, int m, int lane) {
+// x = S^-1 r by refinement with Iv (m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
+// equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i (the warm solve's test),
+// at most kWarmMaxIters corrections, each cutting the error fourfold.  Lane i holds row i of S and of
+// Iv in registers (read once from LDS); the vectors reach every lane by v_readlane with compile-time
+// lanes (the register Gauss-Jordan's broadcast), so a correction is 2m broadcasts and 3m FMAs with
+// no LDS round trip -- round 4's first form read S, Iv and the vectors from LDS per product and took
+// ~3 us at m = 18, longer than the elimination.  On success r holds x.
+template <int MM>
+__device__ __forceinline__ bool small_refine_reg(const double* S, double* r, const double* Iv, int m, int lane) {
     const int li = lane < m ? lane : 0;
-    const double* Sr = S + li * m;
-    const double* Ir = Iv + li * m;
+    double sr[MM], ir[MM];
+#pragma unroll
+    for (int j = 0; j < MM; ++j) {
+        sr[j] = S[li * m + (j < m ? j : 0)];
+        ir[j] = Iv[li * m + (j < m ? j : 0)];
+    }
     const double rr = lane < m ? r[li] : 0.0;
     double x = 0.0;
-    for (int j = 0; j < m; ++j) x = fma(Ir[j], r[j], x);
+#pragma unroll
+    for (int j = 0; j < MM; ++j)
+        if (j < m) x = fma(ir[j], readlane_f64(rr, j), x);
     constexpr double kTol = 64.0 * 1.1102230246251565e-16;
     bool conv = false;
     double qprev = 0.0;
     for (int it = 0;; ++it) {
-        if (lane < 32) xw[lane] = lane < m ? x : 0.0;
-        wave_sync_lds();
         double res = rr, sa = fabs(rr);
-        for (int j = 0; j < m; ++j) {
-            const double sj = Sr[j], xj = xw[j];
-            res = fma(-sj, xj, res);
-            sa = fma(fabs(sj), fabs(xj), sa);
+#pragma unroll
+        for (int j = 0; j < MM; ++j) {
+            if (j < m) {
+                const double xj = readlane_f64(x, j);
+                res = fma(-sr[j], xj, res);
+                sa = fma(fabs(sr[j]), fabs(xj), sa);
+            }
         }
         const double q = lane < m ? (fabs(res) / fmax(sa, 1e-300)) : 0.0;
         const double qm = wave_max(q == q ? q : 1.0);
         conv = qm <= kTol;
         if (conv || it >= kWarmMaxIters || (it > 0 && !(qm <= 0.25 * qprev))) break;
         qprev = qm;
-        if (lane < 32) xw[32 + lane] = lane < m ? res : 0.0;
-        wave_sync_lds();
         double dx = 0.0;
-        for (int j = 0; j < m; ++j) dx = fma(Ir[j], xw[32 + j], dx);
+#pragma unroll
+        for (int j = 0; j < MM; ++j)
+            if (j < m) dx = fma(ir[j], readlane_f64(res, j), dx);
         x += dx;
     }
-    wave_sync_lds();   // every lane has read r before it is overwritten
-    if (conv && lane < m) r[lane] = x;
+    if (conv && lane < m) r[lane] = x;   // rr was read by every lane above (one wave: in order)
     return conv;
+}
+__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, int m, int lane) {
+    switch (m) {
+#define SR(M) case M: return small_refine_reg<M>(S, r, Iv, m, lane);
+        SR(6) SR(12) SR(18) SR(24) SR(30)
+#undef SR
+        default: return false;
+    }
 }
 
 // LARGE: m > 30 (k_solve only: the register-tiled elimination needs the whole workgroup's registers)
@@ -3228,8 +3245,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         if (tid == 64) s_bad_rows = 0;   // (this wave's own write below follows in program order)
         // with the previous system's inverse (k_schur, m <= 30): refinement, else / on failure the
         // register Gauss-Jordan
-        __shared__ double s_xw[64];
-        if (!(Iv && small_refine(S, r, Iv, s_xw, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
+        if (!(Iv && small_refine(S, r, Iv, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
         SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();

@@ -173,16 +173,16 @@ def test_optimize_independent_of_history():
     assert a[2] == b[2] and np.array_equal(a[0], b[0])
 
 
-def test_small_m_warm_opt_in_matches_direct_and_oracle():
-    """The m <= 30 warm solve (MCC_SMALL_WARM=1, opt-in since round 4: slower than the register
-    Gauss-Jordan at m = 18): k_group's spare workgroup inverts the previous step's system and
-    k_schur's final solve refines with it, or eliminates directly when there is no previous system
-    or the refinement does not converge.  Same iterations as the direct path and the oracle, float32
+def test_small_m_warm_matches_direct_and_oracle():
+    """The m <= 30 warm solve (default on k_group -> k_schur; MCC_SMALL_WARM=0 turns it off): k_group's
+    spare workgroup inverts the previous step's system and k_schur's final solve refines with it
+    (S and the inverse in registers), or eliminates directly when there is no previous system or
+    the refinement does not converge.  Same iterations as the direct path and the oracle, float32
     parameters within 1 ulp of both."""
     p = rig.make_config("config4", n_views=200)   # m = 18, k_group -> k_schur
     x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
     xw, mw, itw, _ = run(p, {"MCC_FUSED": "0", "MCC_SMALL_WARM": "1"})
-    xd, md, itd, _ = run(p, {"MCC_FUSED": "0"})
+    xd, md, itd, _ = run(p, {"MCC_FUSED": "0", "MCC_SMALL_WARM": "0"})
     assert itw == itd == it_ref, (itw, itd, it_ref)
     for x, m in ((xw, mw), (xd, md)):
         assert abs(m - m_ref) <= 1e-6
