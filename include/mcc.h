@@ -196,6 +196,14 @@ int mcc_timing_end(mcc_problem *p, double *lin_ms_per_launch, double *step_ms, i
  * is window i's device time (a leading window, which would include the idle gap before the first
  * launch, is run and dropped).  *graph_launched = 1 when the steps ran as graphs. */
 int mcc_timing_windows(mcc_problem *p, int n_windows, int steps, double *ms_per_window, int *graph_launched);
+/* split-step problems: average device time (ms) per launch of the linearisation kernels alone
+ * (k_group, or k_prep + k_edge + k_photo), `launches` of them in ONE captured graph bracketed by two
+ * HIP events on the problem's stream -- the kernels back to back as the step graphs run them, with
+ * no event between them (events recorded inside a captured graph carry no timestamps on HIP).  Each
+ * launch re-applies the pending photo update, so the parameters are restored after the window; the
+ * Schur slots and photo factors then hold a linearisation at those drifted parameters, which the
+ * next steps overwrite (a timing probe, not a step).  MCC_EINVAL for a fused-step problem. */
+int mcc_timing_linearize(mcc_problem *p, int launches, double *ms_per_launch);
 /* average time (ms) of the step's data-path exchange over the same window, and the exchanges:
  * RCCL all-reduces by HIP event pairs around each ncclAllReduce, the peer transport by the
  * device's own s_memrealtime ticks from the first send to the rank-ordered sums (in-kernel, so

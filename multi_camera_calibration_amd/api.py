@@ -112,6 +112,7 @@ def lib():
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_timing_exchange.argtypes = [ctypes.c_void_p, _f64p, _i32p]
         L.mcc_timing_windows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f64p, _i32p]
+        L.mcc_timing_linearize.argtypes = [ctypes.c_void_p, ctypes.c_int, _f64p]
         L.mcc_project_error_detail.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f32p, _f32p,
                                                ctypes.POINTER(ctypes.c_longlong), _f64p]
         L.mcc_problem_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_longlong)] * 4
@@ -347,6 +348,13 @@ class BundleAdjuster:
                                               ctypes.byref(tot), ctypes.byref(npts), ctypes.byref(mean)),
                "mcc_project_error_detail")
         return err, cerr, tot.value, npts.value, mean.value
+
+    def timing_linearize(self, launches: int) -> float:
+        """Split step: ms per launch of the linearisation kernels alone, `launches` of them in one
+        captured graph between two HIP events (mcc_timing_linearize)."""
+        ms = ctypes.c_double()
+        _check(lib().mcc_timing_linearize(self.h, launches, ctypes.byref(ms)), "mcc_timing_linearize")
+        return ms.value
 
     def timing_exchange(self):
         """(ms per data-path exchange, exchanges) over the last timing window (mcc_timing_exchange)."""

@@ -190,7 +190,7 @@ struct mcc_problem {
     // linearises; the next k_solve refines with it (WarmCtx, mcc_internal.h)
     bool warm = false;
     hipStream_t side = nullptr;      // the helper's stream
-    double* sinv = nullptr;          // [M x M] (ordinary memory)
+    double* sinv = nullptr;          // the helper's S^-1, packed upper triangle (ordinary memory)
     double* prev2 = nullptr;         // uncached: [2][prev_stride] k_schur's copies of [S | r] (iteration parity)
     int prev_stride = 0;
     unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
@@ -214,6 +214,10 @@ struct mcc_problem {
     static constexpr int kGraphSteps = 8;
     static constexpr int kGraphSizes = 7;   // up to 64 steps per launch
     hipGraphExec_t gexec[kGraphSizes] = {};
+    // mcc_timing_linearize: a graph of lin_graph_n launches of the split step's linearisation kernels
+    hipGraphExec_t lin_graph = nullptr;
+    int lin_graph_n = 0;
+    DevBuf<float> xsave;   // x across that window (each launch applies the pending photo update again)
     int graph_sizes = kGraphSizes;   // MCC_GRAPH_SIZES (A/B of the launch granularity)
     bool use_graph = true;
     // the device State is in free-running mode (crit_type 0) since the last mcc_step: later
@@ -276,7 +280,15 @@ mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
     return pc;
 }
 
-int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
+// every captured graph of the problem (they hold kernel arguments: buffers, transport, stamps)
+void drop_graphs(mcc_problem* p) {
+    for (auto& g : p->gexec)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    if (p->lin_graph) { (void)hipGraphExecDestroy(p->lin_graph); p->lin_graph = nullptr; }
+}
+
+// lin_only (mcc_timing_linearize): the split step's linearisation kernels alone
+int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only = false) {
     using namespace mcc;
     const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
     // the m <= 30 warm solve (k_group's spare workgroup inverts the previous step's system; k_schur
@@ -346,6 +358,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev) {
         else
             HIPCHK(mcc_launch_linearize(la, p->model, p->V, p->max_epp, p->rational, p->prism, p->stream));
     }
+    if (lin_only) return MCC_OK;
     if (tim) HIPCHK(hipEventRecord(p->ev_lin[p->ev_used + 1], p->stream));
     if (p->fused) {
         if (rccl) {
@@ -991,8 +1004,8 @@ void mcc_destroy(mcc_problem* p) {
     if (p->prev2) (void)hipFree(p->prev2);
     if (p->wsync) (void)hipFree(p->wsync);
     p->warm_stats.release();
-    for (auto& g : p->gexec)
-        if (g) (void)hipGraphExecDestroy(g);
+    drop_graphs(p);
+    p->xsave.release();
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
     for (auto e : p->ev_x) (void)hipEventDestroy(e);
@@ -1249,8 +1262,7 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
         const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + mcc::kSchurStampStride * (size_t)(p->n_items + p->n_norm_chunks) + 16;
         HIPCHK(p->stamps.alloc(n_st));
         HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
-        for (auto& g : p->gexec)
-            if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }   // graphs captured the old pointer
+        drop_graphs(p);   // graphs captured the old pointer
         return MCC_OK;   // armed: the next steps record
     }
     HIPCHK(hipStreamSynchronize(p->stream));
@@ -1365,6 +1377,47 @@ int mcc_timing_windows(mcc_problem* p, int n_windows, int steps, double* ms_per_
     return MCC_OK;
 }
 
+int mcc_timing_linearize(mcc_problem* p, int launches, double* ms_per_launch) {
+    if (!p || launches < 1 || !ms_per_launch) return fail(MCC_EINVAL, "bad arguments");
+    HIPCHK(hipSetDevice(p->device));
+    if (p->fused) return fail(MCC_EINVAL, "mcc_timing_linearize: the fused step is one kernel (mcc_timing_begin / end)");
+    if (p->timing || p->timing_window) return fail(MCC_EINVAL, "mcc_timing_linearize inside a timing window");
+    if (!p->stepping) {
+        int rc = set_state(p, 0, 0, 0, 0.0);
+        if (rc) return rc;
+        p->stepping = true;
+    }
+    if (!p->lin_graph || p->lin_graph_n != launches) {
+        if (p->lin_graph) { (void)hipGraphExecDestroy(p->lin_graph); p->lin_graph = nullptr; }
+        hipGraph_t graph;
+        HIPCHK(hipStreamBeginCapture(p->stream, hipStreamCaptureModeThreadLocal));
+        int rc = MCC_OK;
+        for (int i = 0; i < launches && rc == MCC_OK; ++i) rc = enqueue_step(p, 1, nullptr, true);
+        hipError_t ee = hipStreamEndCapture(p->stream, &graph);
+        if (rc != MCC_OK) return rc;
+        if (ee != hipSuccess) return fail(MCC_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ee));
+        HIPCHK(hipGraphInstantiate(&p->lin_graph, graph, nullptr, nullptr, 0));
+        HIPCHK(hipGraphDestroy(graph));
+        p->lin_graph_n = launches;
+    }
+    if (!p->ev_win[0]) {
+        HIPCHK(hipEventCreate(&p->ev_win[0]));
+        HIPCHK(hipEventCreate(&p->ev_win[1]));
+    }
+    if (!p->xsave.p) HIPCHK(p->xsave.alloc(p->P));
+    HIPCHK(hipMemcpyAsync(p->xsave.p, p->x.p, sizeof(float) * p->P, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipEventRecord(p->ev_win[0], p->stream));
+    HIPCHK(hipGraphLaunch(p->lin_graph, p->stream));
+    HIPCHK(hipEventRecord(p->ev_win[1], p->stream));
+    // the parameters as before the window (each launch re-applied the pending photo update)
+    HIPCHK(hipMemcpyAsync(p->x.p, p->xsave.p, sizeof(float) * p->P, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p->ev_win[0], p->ev_win[1]));
+    *ms_per_launch = ms / launches;
+    return MCC_OK;
+}
+
 int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges) {
     if (!p) return fail(MCC_EINVAL, "null problem");
     HIPCHK(hipSetDevice(p->device));
@@ -1426,8 +1479,7 @@ int mcc_comm_init(mcc_problem* p, const unsigned char* id, int nranks, int rank)
     if (r != ncclSuccess) return fail(MCC_ECOMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     p->nranks = nranks;
     p->rank = rank;
-    for (auto& g : p->gexec)
-        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    drop_graphs(p);
     return MCC_OK;
 }
 
@@ -1518,8 +1570,7 @@ int mcc_peer_init(mcc_problem* p, const unsigned char* handles, int nranks, int 
                                    std::to_string((int)out[3]));
     }
     p->peer_on = true;
-    for (auto& g : p->gexec)
-        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    drop_graphs(p);
     return MCC_OK;
 }
 
@@ -1529,8 +1580,7 @@ int mcc_peer_enable(mcc_problem* p, int on) {
     if (!on && !p->comm && p->peer_n > 1) return fail(MCC_EINVAL, "no RCCL communicator to fall back to");
     if (p->peer_on != (on != 0)) {
         HIPCHK(hipStreamSynchronize(p->stream));
-        for (auto& g : p->gexec)
-            if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+        drop_graphs(p);
     }
     p->peer_on = on != 0;
     return MCC_OK;

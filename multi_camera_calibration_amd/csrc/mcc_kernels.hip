@@ -790,6 +790,18 @@ __device__ __forceinline__ void packed_ij(int t, int m, int& i, int& j) {
     i = row;
     j = row + rem;
 }
+// the same in closed form (no loop: row i starts at i m - i (i - 1) / 2; a float root, then at most
+// one step either way), for m <= 128
+__device__ __forceinline__ void packed_ij_fast(int t, int m, int& i, int& j) {
+    const float b = 2.0f * m + 1.0f;
+    int r = (int)((b - sqrtf(fmaxf(b * b - 8.0f * (float)t, 0.0f))) * 0.5f);
+    r = r < 0 ? 0 : (r > m - 1 ? m - 1 : r);
+    const int s0 = r * m - r * (r - 1) / 2;
+    if (s0 > t) --r;
+    else if (t >= s0 + (m - r)) ++r;
+    i = r;
+    j = r + (t - (r * m - r * (r - 1) / 2));
+}
 
 // sum_{q < n} p[q * stride] in q order with sc1 loads issued 24 at a time (one memory round
 // trip for the group sizes of a few hundred to ~600 photos)
@@ -2910,11 +2922,12 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     if (early && use <= 0 && tid == 0) st_sys_u32(w.sync, e + 1u);
     bool solved = false;
     if (use > 0) {
-        // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
-        // rows of S_{t+1} from the staged packed system; then S_t^-1 into LDS, rows padded to
-        // M + 2 (16 rows of a wave would otherwise share banks)
-        constexpr int kIvPer = 9;   // double2 per thread: M x M / 2 <= 4 608 at 512 threads
-        const int n2i = M * M / 2;
+        // S_t^-1's packed upper triangle (the helper's; one memory round trip, 33 KB at m = 90 instead
+        // of the full 74 KB) into registers; meanwhile the refinement gathers its rows of S_{t+1} from
+        // the staged packed system; then S_t^-1 mirrored into LDS, rows padded to M + 2 (16 rows of a
+        // wave would otherwise share banks; the padding is never read)
+        constexpr int kIvPer = 5;   // double2 per thread: m (m + 1) / 4 <= 2 328 at 512 threads (m <= 96)
+        const int ntri = m * (m + 1) / 2, n2i = (ntri + 1) / 2;
         double2 iv[kIvPer];
 #pragma unroll
         for (int u = 0; u < kIvPer; ++u) {
@@ -2927,9 +2940,16 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
 #pragma unroll
         for (int u = 0; u < kIvPer; ++u) {
             const int q = u * (int)blockDim.x + tid;
-            if (q < n2i) {
-                const int t = 2 * q, r = t / M, c = t % M;
-                *reinterpret_cast<double2*>(Iv + r * (M + 2) + c) = iv[u];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int t = 2 * q + h;
+                if (q < n2i && t < ntri) {
+                    int r, c;
+                    packed_ij_fast(t, m, r, c);
+                    const double v = h ? iv[u].y : iv[u].x;
+                    Iv[r * (M + 2) + c] = v;
+                    Iv[c * (M + 2) + r] = v;
+                }
             }
         }
         lds_barrier();
@@ -3044,10 +3064,18 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         }
         __syncthreads();
         const bool ok = gj_inverse_blocked(A, PV, M);
-        for (int q = tid; q < M * M / 2; q += blockDim.x) {
-            const int t = 2 * q, i = t / M, j = t % M;
-            *reinterpret_cast<double2*>(w.sinv + t) =
-                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(A[i * ld + j], A[i * ld + j + 1]);
+        // S^-1's upper triangle, packed like the system (k_solve mirrors it: half the bytes it loads)
+        for (int q = tid; q < n2; q += blockDim.x) {
+            double v2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int t = 2 * q + h;
+                int i = 0, j = 0;
+                if (t < ntri) packed_ij_fast(t, m, i, j);
+                v2[h] = t < ntri ? A[i * ld + j] : 0.0;
+            }
+            *reinterpret_cast<double2*>(w.sinv + 2 * q) =
+                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(v2[0], v2[1]);
         }
         if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
         // sinv is ordinary (cached) memory: write this XCD's L2 back before the epoch says it is there

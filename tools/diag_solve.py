@@ -31,8 +31,11 @@ for r in range(reps):
     st = ba.stamps()
     rows.append(st)
 ba.close()
-# k_solve's row is the last 16 entries of the stamp buffer (mcc_debug_stamps' layout)
-base = len(rows[-1]) - 16
+# k_solve's row is the last 16-slot row of the device buffer (after k_linearize's 32-slot rows per
+# photo and k_schur's 16-slot rows; mcc_debug_stamps' layout): the row of the last nonzero stamp
+nv = max(p.n_photos, 1)
+last = int(np.nonzero(rows[-1])[0].max())
+base = 32 * nv + 16 * ((last - 32 * nv) // 16)
 labels = {0: "entry", 4: "loads+epochs", 8: "staged", 9: "Sinv in LDS", 10: "refined", 11: "after GJ",
           5: "solved", 6: "update"}
 order = [0, 4, 8, 9, 10, 11, 5, 6]
