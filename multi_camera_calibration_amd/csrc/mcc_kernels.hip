@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     auto place = [&](int t, double v) {
         if (t < ntri) {
             int i, j;
-            packed_ij(t, m, i, j);
+            packed_ij_fast(t, m, i, j);
             S[i * m + j] = v;
             S[j * m + i] = v;
         } else if (t < ntri + m) {
