@@ -190,7 +190,7 @@ struct mcc_problem {
     // linearises; the next k_solve refines with it (WarmCtx, mcc_internal.h)
     bool warm = false;
     hipStream_t side = nullptr;      // the helper's stream
-    double* sinv = nullptr;          // the helper's S^-1, packed upper triangle (ordinary memory)
+    double* sinv = nullptr;          // [M x M] the helper's S^-1 (ordinary memory)
     double* prev2 = nullptr;         // uncached: [2][prev_stride] k_schur's copies of [S | r] (iteration parity)
     int prev_stride = 0;
     unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag

@@ -261,7 +261,7 @@ struct SchurArgs {
 // inverse, and a helper that does not deliver within wait_ticks fails the step (error bit 3,
 // MCC_ETIMEOUT) instead of switching to the direct elimination.
 struct WarmCtx {
-    double* sinv;            // the helper's inverse, upper triangle packed like the system (row-major, ntri doubles)
+    double* sinv;            // [M x M] (M = 16 ceil(m / 16), row-major) the helper's inverse
     int* sinv_ok_sys;        // the helper's elimination found the system positive definite
     double* prev2;           // [2][prev_stride] uncached: the copy of [S | r] per iteration parity
     int prev_stride;         // packed [S | r] rounded up to even

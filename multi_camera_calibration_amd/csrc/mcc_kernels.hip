@@ -2922,12 +2922,12 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     if (early && use <= 0 && tid == 0) st_sys_u32(w.sync, e + 1u);
     bool solved = false;
     if (use > 0) {
-        // S_t^-1's packed upper triangle (the helper's; one memory round trip, 33 KB at m = 90 instead
-        // of the full 74 KB) into registers; meanwhile the refinement gathers its rows of S_{t+1} from
-        // the staged packed system; then S_t^-1 mirrored into LDS, rows padded to M + 2 (16 rows of a
-        // wave would otherwise share banks; the padding is never read)
-        constexpr int kIvPer = 5;   // double2 per thread: m (m + 1) / 4 <= 2 328 at 512 threads (m <= 96)
-        const int ntri = m * (m + 1) / 2, n2i = (ntri + 1) / 2;
+        // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
+        // rows of S_{t+1} from the staged packed system; then S_t^-1 into LDS, rows padded to
+        // M + 2 (16 rows of a wave would otherwise share banks).  (Its packed upper triangle, half
+        // the bytes, was slower: mirroring it into LDS cost more than the saved load, round 4.)
+        constexpr int kIvPer = 9;   // double2 per thread: M x M / 2 <= 4 608 at 512 threads
+        const int n2i = M * M / 2;
         double2 iv[kIvPer];
 #pragma unroll
         for (int u = 0; u < kIvPer; ++u) {
@@ -2940,16 +2940,9 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
 #pragma unroll
         for (int u = 0; u < kIvPer; ++u) {
             const int q = u * (int)blockDim.x + tid;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int t = 2 * q + h;
-                if (q < n2i && t < ntri) {
-                    int r, c;
-                    packed_ij_fast(t, m, r, c);
-                    const double v = h ? iv[u].y : iv[u].x;
-                    Iv[r * (M + 2) + c] = v;
-                    Iv[c * (M + 2) + r] = v;
-                }
+            if (q < n2i) {
+                const int t = 2 * q, r = t / M, c = t % M;
+                *reinterpret_cast<double2*>(Iv + r * (M + 2) + c) = iv[u];
             }
         }
         lds_barrier();
@@ -3064,18 +3057,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         }
         __syncthreads();
         const bool ok = gj_inverse_blocked(A, PV, M);
-        // S^-1's upper triangle, packed like the system (k_solve mirrors it: half the bytes it loads)
-        for (int q = tid; q < n2; q += blockDim.x) {
-            double v2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int t = 2 * q + h;
-                int i = 0, j = 0;
-                if (t < ntri) packed_ij_fast(t, m, i, j);
-                v2[h] = t < ntri ? A[i * ld + j] : 0.0;
-            }
-            *reinterpret_cast<double2*>(w.sinv + 2 * q) =
-                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(v2[0], v2[1]);
+        for (int q = tid; q < M * M / 2; q += blockDim.x) {
+            const int t = 2 * q, i = t / M, j = t % M;
+            *reinterpret_cast<double2*>(w.sinv + t) =
+                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(A[i * ld + j], A[i * ld + j + 1]);
         }
         if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
         // sinv is ordinary (cached) memory: write this XCD's L2 back before the epoch says it is there
