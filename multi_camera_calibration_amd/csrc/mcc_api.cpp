@@ -291,16 +291,18 @@ void drop_graphs(mcc_problem* p) {
 int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only = false) {
     using namespace mcc;
     const bool tim = p->timing && p->ev_used + 2 <= (int)p->ev_lin.size();
-    // the m <= 30 warm solve (k_group's spare workgroup inverts the previous step's system; k_schur
-    // refines with it): single GPU or the peer transport (with RCCL, k_solve solves)
+    // the m <= 30 warm solve (a spare workgroup of k_group / k_linearize inverts the previous step's
+    // system; k_schur's or the next k_linearize's final arriver refines with it): single GPU or the
+    // peer transport (with RCCL, k_solve solves)
     const bool swarm = p->ssinv.p && (p->peer_on || !p->comm);
     if (p->poison) {
         // (with the warm solve the packed system carries the previous step's system into the next
-        // step, like dg: it is an input of the step, not a hand-off inside it, and stays unpoisoned)
+        // step, like dg: it is an input of the step, not a hand-off inside it, and stays unpoisoned;
+        // on the fused step so does the inverse, which the next launch reads)
         for (auto* b : {&p->contrib, &p->gsum, &p->item_out, &p->pairprod, &p->packed, &p->ssinv})
-            if (b->p && b->n && !(swarm && b == &p->packed))
+            if (b->p && b->n && !(swarm && b == &p->packed) && !(p->fused && b == &p->ssinv))
                 HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
-        if (swarm) HIPCHK(hipMemsetAsync(p->ssinv_ok.p, 0xFF, sizeof(int), p->stream));
+        if (swarm && !p->fused) HIPCHK(hipMemsetAsync(p->ssinv_ok.p, 0xFF, 2 * sizeof(int), p->stream));
         for (auto* b : {&p->erec, &p->echain, &p->eh})
             if (b->p && b->n) HIPCHK(hipMemsetAsync(b->p, 0xFF, sizeof(double) * b->n, p->stream));
         // 2: the negative control -- dg carries the previous solve into this step's photo update,
@@ -956,14 +958,19 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // only).  With S and the inverse in registers the refinement takes ~1.7 us at m = 18 against the
     // elimination's ~2.6 (config4, interleaved: 28.9 vs 29.4 us per step); round 4's first form, reading
     // them from LDS per product, took ~3 us and lost
+    // The fused step (config2) refines with the inverse its previous launch's spare workgroup formed
+    // (two updates stale: the spare and the final arriver of one launch run at the same time); its
+    // LDS holds the spare's [S | I] and the final arriver's S, r and inverse (mcc_lin_shmem).
+    // Two buffers by iteration parity, each tagged with the iteration that made it.
     {
-        bool sw = !p->fused && p->use_group && p->schur_one_level &&
-                  p->group_shmem >= (size_t)2 * p->m * p->m * sizeof(double);   // the spare's [S | I] in LDS
+        bool sw = (!p->fused && p->use_group && p->schur_one_level &&
+                   p->group_shmem >= (size_t)2 * p->m * p->m * sizeof(double)) ||   // the spare's [S | I] in LDS
+                  (p->fused && p->m <= 30);
         if (const char* f = std::getenv("MCC_SMALL_WARM")) sw = sw && std::atoi(f) != 0;
         if (sw) {
-            HIPC(p->ssinv.alloc((size_t)p->m * p->m));
-            HIPC(p->ssinv_ok.alloc(1));
-            HIPC(hipMemset(p->ssinv_ok.p, 0, sizeof(int)));
+            HIPC(p->ssinv.alloc(2 * (size_t)p->m * p->m));
+            HIPC(p->ssinv_ok.alloc(2));
+            HIPC(hipMemset(p->ssinv_ok.p, 0, 2 * sizeof(int)));
         }
     }
     p->warm = !p->fused && p->m > 30;

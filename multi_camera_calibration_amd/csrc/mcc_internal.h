@@ -114,8 +114,8 @@ struct LinArgs {
     int fault_photo;         // test (MCC_FAULT_PHOTO): this local photo's 6 x 6 block is reported not
                              // positive definite (its factor stays finite); -1 off
     // m <= 30 warm solve: k_group's spare workgroup inverts the previous step's packed system
-    double* ssinv;           // [m x m] (null: off)
-    int* ssinv_ok;           // 1: ssinv holds the previous update step's inverse
+    double* ssinv;           // [2][m x m] by iteration parity (null: off)
+    int* ssinv_ok;           // [2] the iteration + 1 whose spare workgroup formed the buffer (0: none)
 };
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
@@ -235,8 +235,8 @@ struct SchurArgs {
     double* packed;
     int m, rank, fuse_solve;
     int one_level;       // m <= 30: one hand-off level (schur_one_level) instead of items -> blocks -> norms
-    const double* ssinv; // m <= 30 warm solve: the previous system's inverse (k_group's spare workgroup)
-    const int* ssinv_ok;
+    const double* ssinv; // m <= 30 warm solve: [2][m x m], this step's in buffer iteration & 1 (k_group's spare)
+    const int* ssinv_ok; // [2] tags (iteration + 1)
     SolveCtx solve;
     long long* stamps;   // MCC_DIAG builds: [8 * grid]
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves

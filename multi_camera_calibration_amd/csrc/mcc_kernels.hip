@@ -914,6 +914,7 @@ __device__ __forceinline__ double photo_flag_norm(int err, int w, double v) {
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
                                              const WarmCtx* warm = nullptr, const double* Iv = nullptr);
+__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A);
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
@@ -923,6 +924,11 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     State* st = a.state;
     const int photo = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    if (photo == a.n_photos) {   // the spare workgroup (a.ssinv): the previous system's inverse
+        if (!st->done) small_inverse(a, smem);
+        return;
+    }
     // ---- round trip 1: everything indexed by the photo alone
     const int done = st->done, pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update
@@ -939,7 +945,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         a.stamps[kStampStride * (size_t)photo + 27] = ne;
     }
 #endif
-    extern __shared__ __attribute__((aligned(16))) double smem[];
     EdgeLds* el = reinterpret_cast<EdgeLds*>(smem);
     PhotoLds& P = *reinterpret_cast<PhotoLds*>(smem + (size_t)ne * (sizeof(EdgeLds) / sizeof(double)));
     double* ctab = reinterpret_cast<double*>(&P + 1);   // [C][kCamStride] = {R, Jl, T}
@@ -1336,7 +1341,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     RSTAMP(29);
     // ---- level 1: the last photo of a group sums the group in photo order
     const int G = a.group_size, grp = photo / G, g0 = grp * G;
-    const int gn = min(G, (int)gridDim.x - g0);
+    const int gn = min(G, a.n_photos - g0);   // (the grid may carry the warm solve's spare workgroup)
     const bool grp_last = arrive_last_sc1(a.cnt + grp, gn, a.stamps ? a.stamps + kStampStride * (size_t)photo + 28 : nullptr);
     // the next step's pending-update matrix of this photo (after the ticket: off its drain),
     // W[k][6g + i] = sum over the photo's edges e of camera block g of Y'_e[i][k]
@@ -1382,10 +1387,20 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         }
     };
     const bool peer = a.peer.nranks > 0;
-    const int err_now = photo_error(st);   // issued ahead of the group sums' loads
-    for (int t = tid; t < Lc; t += blockDim.x) {
-        double v = 0.0;
-        v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
+    // the m <= 30 warm solve: the inverse the previous launch's spare workgroup formed (of the system
+    // two updates back: this launch's spare is still inverting the last one), loaded with the group
+    // sums; used when its tag says which iteration made it (small_inverse)
+    constexpr int kIvF = 4;   // m^2 <= 900 doubles over 256 threads
+    double ivv[kIvF];
+    int ivtag = 0;
+    const bool ivuse = a.ssinv && a.fuse_solve && iter0 >= 1;
+    if (ivuse) {
+        const double* src = a.ssinv + (size_t)((iter0 - 1) & 1) * m * m;
+        ivtag = a.ssinv_ok[(iter0 - 1) & 1];
+#pragma unroll
+        for (int u = 0; u < kIvF; ++u) ivv[u] = src[min(u * (int)blockDim.x + tid, m * m - 1)];
+    }
+    auto finish_entry = [&](int t, double v, int err) {
         if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
             const int w = t - ntri - 2 * m;
             if (iter0 > 0) {
@@ -1393,10 +1408,30 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             } else {
                 v = 0.0;
             }
-            v = photo_flag_norm(err_now, w, v);
+            v = photo_flag_norm(err, w, v);
         }
         if (!peer) place(t, v);
         a.packed[t] = v;
+    };
+    if (Lc <= (int)blockDim.x && a.n_groups <= 24) {
+        // one entry per thread (m <= 18), its column of group sums in one batch of loads with no
+        // loop around it: a loop's head would wait for the inverse's loads above first
+        const int ng = a.n_groups, tt = min(tid, Lc - 1);
+        double b[24];
+#pragma unroll
+        for (int q = 0; q < 24; ++q) b[q] = ld_sc1(a.gsum + (size_t)min(q, ng - 1) * Lcp + tt);
+        // the error word after the sums' loads: the compiler makes it uniform (v_readfirstlane) and
+        // waits for it at once, which in front of the batch would be a memory round trip of its own
+        const int err_now = photo_error(st);
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < 24; ++q) v += q < ng ? b[q] : 0.0;   // group order (sum_sc1's additions)
+        if (tid < Lc) finish_entry(tid, v, err_now);
+    } else {
+        for (int t = tid; t < Lc; t += blockDim.x) {
+            const double v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
+            finish_entry(t, v, photo_error(st));
+        }
     }
     STAMP(17);   // thread 0's share of the assembly done (MCC_DIAG)
     if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
@@ -1404,13 +1439,23 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);
     }
     if (!a.fuse_solve) { RSTAMP(15); return; }
+    double* Iv = smem + m * m + m;   // after S and rr (the host sizes the LDS for it)
+    __shared__ int iv_ok;
+    if (ivuse) {
+#pragma unroll
+        for (int u = 0; u < kIvF; ++u) {
+            const int t = u * (int)blockDim.x + tid;
+            if (t < m * m) Iv[t] = ivv[u];
+        }
+        if (tid == 0) iv_ok = ivtag == iter0;
+    }
     __syncthreads();
     STAMP(12);
     SolveCtx sc = a.solve;
 #ifdef MCC_DIAG
     sc.stamps = a.stamps ? a.stamps + kStampStride * (size_t)photo + 20 : nullptr;   // slots 20..26
 #endif
-    solve_global<false>(sc, S, rr, nrm2[0], nrm2[1]);
+    solve_global<false>(sc, S, rr, nrm2[0], nrm2[1], nullptr, ivuse && iv_ok ? Iv : nullptr);
     STAMP(13);
     RSTAMP(15);
 }
@@ -3105,9 +3150,14 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
     const State* st = a.state;
     const int tid = threadIdx.x, nt = blockDim.x, m = a.global_dim, W = 2 * m;
+    // buffer iteration & 1, tagged iteration + 1 (0: none): k_schur of this step reads it, the fused
+    // step's final arriver of the NEXT launch does (this launch's is still inverting)
+    const int it = st->iter, pend = st->pending;
+    double* out = a.ssinv + (size_t)(it & 1) * m * m;
+    int* okp = a.ssinv_ok + (it & 1);
     __shared__ int ok_s;
-    if (!st->pending) {   // no update step before this one: no system to precondition with
-        if (tid == 0) a.ssinv_ok[0] = 0;
+    if (!pend) {   // no update step before this one: no system to precondition with
+        if (tid == 0) *okp = 0;
         return;
     }
     for (int t = tid; t < m * W; t += nt) {
@@ -3146,9 +3196,9 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
     if (ok)
         for (int t = tid; t < m * m; t += nt) {
             const int i = t / m, j = t % m;
-            a.ssinv[t] = A[i * W + m + j] / A[i * W + i];
+            out[t] = A[i * W + m + j] / A[i * W + i];
         }
-    if (tid == 0) a.ssinv_ok[0] = ok ? 1 : 0;
+    if (tid == 0) *okp = ok ? it + 1 : 0;
 }
 
 // x = S^-1 r by refinement with Iv (m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
@@ -3367,7 +3417,7 @@ constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <
 // independent unconditional loads: a load under a per-item condition, or a loop whose stores wait
 // on its loads, costs a round trip per load or iteration: 5 us at config4 in the first form), and
 // the sums are formed from LDS.
-__device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
+__device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) {
     State* st = a.state;
     const int tid = threadIdx.x;
     if (!arrive_last_sc1(a.counter, (int)gridDim.x)) return;
@@ -3389,7 +3439,9 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
     const int iter = st->iter;
     const double cn0 = st->cam_normG2, cn1 = st->cam_normX2;
     const int err_now = photo_error(st);
-    const int ivok = Iv ? a.ssinv_ok[0] : 0;
+    // this step's spare workgroup inverted the previous system into buffer iter & 1, tagged iter + 1
+    const double* ivsrc = a.ssinv ? a.ssinv + (size_t)(iter_e & 1) * m * m : nullptr;
+    const int ivok = Iv ? a.ssinv_ok[iter_e & 1] == iter_e + 1 : 0;
     {
         // one batch of U loads per thread, no loop (a loop's header waits for the previous iteration's
         // loads, and so for the state loads above), U the smallest of 4 / 8 / 16 that covers n: a
@@ -3404,7 +3456,7 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a) {
             for (int u = 0; u < U; ++u) {
                 int t = u * kSchurThreads + tid;
                 t = t < n ? t : n - 1;
-                v[u] = ld_sc1(t < nI ? a.item_out + t : a.ssinv + (t - nI));
+                v[u] = ld_sc1(t < nI ? a.item_out + t : ivsrc + (t - nI));
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -3509,7 +3561,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
     // the warm solve's copy of this step's [S | r] (m > 30): prev2[iteration & 1] (same cache line as done)
-    double* prev = a.prev2 ? a.prev2 + (size_t)(st->iter & 1) * a.prev_stride : nullptr;
+    const int iter_e = st->iter;
+    double* prev = a.prev2 ? a.prev2 + (size_t)(iter_e & 1) * a.prev_stride : nullptr;
     STAMPP(a.stamps, kSchurStampStride, 0);
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
@@ -3563,7 +3616,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     }
     STAMPP(a.stamps, kSchurStampStride, 1);
     if (a.one_level) {
-        schur_one_level(a);
+        schur_one_level(a, iter_e);
         return;
     }
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
@@ -3922,10 +3975,11 @@ using namespace mcc;
 
 template <int MODEL>
 static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
-    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), dim3(n_photos), dim3(256), shmem, s, a);
-    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), dim3(n_photos), dim3(256), shmem, s, a);
-    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), dim3(n_photos), dim3(256), shmem, s, a);
+    const dim3 grid(n_photos + (a.ssinv ? 1 : 0));   // + the m <= 30 warm solve's spare workgroup
+    if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), grid, dim3(256), shmem, s, a);
+    else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), grid, dim3(256), shmem, s, a);
+    else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), grid, dim3(256), shmem, s, a);
+    else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), grid, dim3(256), shmem, s, a);
     return hipGetLastError();
 }
 
@@ -3977,7 +4031,8 @@ size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
                        (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
                        ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15);
-    return std::max(lin, (size_t)(m * m + m) * sizeof(double));
+    // the final arriver's S, r and the warm solve's inverse; the spare workgroup's [S | I]
+    return std::max(lin, (size_t)(2 * m * m + m) * sizeof(double));
 }
 
 size_t mcc_solve_shmem(int m) {

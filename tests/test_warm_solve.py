@@ -173,16 +173,20 @@ def test_optimize_independent_of_history():
     assert a[2] == b[2] and np.array_equal(a[0], b[0])
 
 
-def test_small_m_warm_matches_direct_and_oracle():
-    """The m <= 30 warm solve (default on k_group -> k_schur; MCC_SMALL_WARM=0 turns it off): k_group's
-    spare workgroup inverts the previous step's system and k_schur's final solve refines with it
-    (S and the inverse in registers), or eliminates directly when there is no previous system or
-    the refinement does not converge.  Same iterations as the direct path and the oracle, float32
-    parameters within 1 ulp of both."""
-    p = rig.make_config("config4", n_views=200)   # m = 18, k_group -> k_schur
+@pytest.mark.parametrize("cfg,views,env", [
+    ("config4", 200, {"MCC_FUSED": "0"}),   # k_group -> k_schur: this step's spare workgroup's inverse
+    ("config2", 120, {}),                   # the fused step: the previous launch's (two updates stale)
+])
+def test_small_m_warm_matches_direct_and_oracle(cfg, views, env):
+    """The m <= 30 warm solve (default; MCC_SMALL_WARM=0 turns it off): a spare workgroup inverts the
+    previous step's system and the final solve refines with it (S and the inverse in registers), or
+    eliminates directly when there is no inverse of the right iteration or the refinement does not
+    converge.  Same iterations as the direct path and the oracle, float32 parameters within 1 ulp of
+    both."""
+    p = rig.make_config(cfg, n_views=views)   # m = 18
     x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
-    xw, mw, itw, _ = run(p, {"MCC_FUSED": "0", "MCC_SMALL_WARM": "1"})
-    xd, md, itd, _ = run(p, {"MCC_FUSED": "0", "MCC_SMALL_WARM": "0"})
+    xw, mw, itw, _ = run(p, dict(env, MCC_SMALL_WARM="1"))
+    xd, md, itd, _ = run(p, dict(env, MCC_SMALL_WARM="0"))
     assert itw == itd == it_ref, (itw, itd, it_ref)
     for x, m in ((xw, mw), (xd, md)):
         assert abs(m - m_ref) <= 1e-6
