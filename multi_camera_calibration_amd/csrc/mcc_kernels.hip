@@ -4031,8 +4031,9 @@ size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
                        (kCamStride + kIntrStride) * sizeof(double) * (size_t)n_cams +
                        ((5 * sizeof(float) * (size_t)max_cpp + 15) & ~(size_t)15);
-    // the final arriver's S, r and the warm solve's inverse; the spare workgroup's [S | I]
-    return std::max(lin, (size_t)(2 * m * m + m) * sizeof(double));
+    // the final arriver's S, r and (m <= 30, the fused step) the warm solve's inverse; the spare
+    // workgroup's [S | I]
+    return std::max(lin, (size_t)((m <= 30 ? 2 : 1) * m * m + m) * sizeof(double));
 }
 
 size_t mcc_solve_shmem(int m) {
