@@ -2951,18 +2951,6 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     double* Iv = Pk + 2 * n2;                        // staged S_t^-1
     double* work = Iv + (size_t)M * (M + 2);
     double* prev = w.prev2 + (size_t)(e & 1u) * w.prev_stride;   // iteration e's copy
-    // S_t^-1 (the largest load, one memory round trip) issued before the staging: the stop test
-    // already read the epoch that says the helper wrote it
-    constexpr int kIvPer = 9;   // double2 per thread: M x M / 2 <= 4 608 at 512 threads
-    const int n2i = M * M / 2;
-    double2 iv[kIvPer];
-    if (use > 0) {
-#pragma unroll
-        for (int u = 0; u < kIvPer; ++u) {
-            const int q = u * (int)blockDim.x + tid;
-            iv[u] = q < n2i ? reinterpret_cast<const double2*>(w.sinv)[q] : make_double2(0.0, 0.0);
-        }
-    }
 #pragma unroll
     for (int u = 0; u < kWarmPer; ++u) {
         const int q = u * (int)blockDim.x + tid;
@@ -2979,10 +2967,18 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     if (early && use <= 0 && tid == 0) st_sys_u32(w.sync, e + 1u);
     bool solved = false;
     if (use > 0) {
-        // S_t^-1 is in flight (above); meanwhile the refinement gathers its rows of S_{t+1} from
-        // the staged packed system; then S_t^-1 into LDS, rows padded to M + 2 (16 rows of a wave
-        // would otherwise share banks).  (Its packed upper triangle, half the bytes, was slower:
-        // mirroring it into LDS cost more than the saved load, round 4.)
+        // S_t^-1 (one memory round trip) into registers; meanwhile the refinement gathers its
+        // rows of S_{t+1} from the staged packed system; then S_t^-1 into LDS, rows padded to
+        // M + 2 (16 rows of a wave would otherwise share banks).  (Its packed upper triangle, half
+        // the bytes, was slower: mirroring it into LDS cost more than the saved load, round 4.)
+        constexpr int kIvPer = 9;   // double2 per thread: M x M / 2 <= 4 608 at 512 threads
+        const int n2i = M * M / 2;
+        double2 iv[kIvPer];
+#pragma unroll
+        for (int u = 0; u < kIvPer; ++u) {
+            const int q = u * (int)blockDim.x + tid;
+            iv[u] = q < n2i ? reinterpret_cast<const double2*>(w.sinv)[q] : make_double2(0.0, 0.0);
+        }
         lds_barrier();   // the staged packed system
         double Sr[kWarmQ];
         warm_gather_s(Pk, m, Sr);
