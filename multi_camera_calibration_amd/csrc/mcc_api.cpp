@@ -776,11 +776,12 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // doubles; item = {block, first slot's offset, slots, slot size}
     int n_slots = 0;
     size_t n_doubles = 0;
-    // m <= 30 (one hand-off level: the final arriver loads every item's partial in one batch, so
-    // more items cost it little): 64 slots per item, four items per 250-slot block at config4 --
-    // 28.6-28.8 vs 29.1-29.3 us per step with 320 (interleaved, round 4; 32: 28.7-28.8, 16: 30.7;
-    // config5 equal at 64, slower at 32)
-    int min_slots = p->m <= 30 ? 64 : 320;
+    // m <= 30 with several camera-pair blocks (one hand-off level: the final arriver loads every
+    // item's partial in one batch, so more items cost it little): 64 slots per item, four items per
+    // 250-slot block at config4 -- 28.4-28.6 vs 29.1-29.2 us per step with 320 (interleaved, round 4;
+    // 32: 28.7-28.8, 16: 30.7).  config5's single block (DoubleSide, m = 6) keeps 320 (60.5-60.7 vs
+    // 60.8-60.9 at 64)
+    int min_slots = p->m <= 30 && p->nblk > 1 ? 64 : 320;
     if (const char* f = std::getenv("MCC_ITEM_SLOTS")) min_slots = std::max(1, std::atoi(f));
     for (int b = 0; b < p->nblk; ++b) {
         int b1 = 0;
