@@ -3567,7 +3567,6 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
     __shared__ double part[kSub][48];
-    __shared__ double red[256];
     if (item < a.n_items) {
         const int4 it = a.items[item];   // {block, first slot's offset (doubles), slots, slot size 48 | 36 [| single]}
         const int q = tid % 48, sub = tid / 48, sz = it.w & (kItemSingle - 1);
@@ -3601,17 +3600,23 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
             else st_sc1(a.item_out + 48 * (size_t)item + tid, t);
         }
     } else {
+        // a norm chunk: 256 photos' ||G||^2, ||x||^2 partials, both in one round trip and a fixed
+        // butterfly per wave (wave_sum), the four waves in order (round 3's LDS tree took 18 barriers)
         const int c = item - a.n_items;
-        const int p = c * 256 + tid;
-        for (int w = 0; w < 2; ++w) {
-            red[tid] = p < a.n_photos ? a.photo_norm[2 * (size_t)p + w] : 0.0;
-            __syncthreads();
-            for (int o = 128; o >= 1; o >>= 1) {
-                if (tid < o) red[tid] += red[tid + o];
-                __syncthreads();
-            }
-            if (tid == 0) st_sc1(a.item_out + 48 * (size_t)item + w, red[0]);
-            __syncthreads();
+        const int p = c * 256 + tid, pc = min(p, a.n_photos - 1);
+        const double2 gx = *reinterpret_cast<const double2*>(a.photo_norm + 2 * (size_t)pc);
+        const double g = wave_sum(p < a.n_photos ? gx.x : 0.0), x = wave_sum(p < a.n_photos ? gx.y : 0.0);
+        __shared__ double wred[2][kSchurThreads / 64];
+        if ((tid & 63) == 0) {
+            wred[0][tid >> 6] = g;
+            wred[1][tid >> 6] = x;
+        }
+        __syncthreads();
+        if (tid < 2) {
+            double v = 0.0;
+#pragma unroll
+            for (int w = 0; w < kSchurThreads / 64; ++w) v += wred[tid][w];
+            st_sc1(a.item_out + 48 * (size_t)item + tid, v);
         }
     }
     STAMPP(a.stamps, kSchurStampStride, 1);
