@@ -1,4 +1,5 @@
 #!/bin/bash
+# (interleaved A/B trees: tools/mk_ab_tree.sh NAME COMMIT builds build_ab/NAME from an older commit)
 # Interleaved bench.py ms/step over several trees under build_ab/<name> and this tree (HEAD):
 #   tools/ab_trees.sh CONFIG ROUNDS NAME... [HEAD] ["HEAD:VAR=a ..."]
 set -o pipefail
