@@ -220,8 +220,10 @@ def workload_label(name: str, views_per_rank: int, world: int) -> str:
             f"views{per} (BASELINE.json configs[{CONFIG_INDEX[name]}]), one Gauss-Newton step per 'step'")
 
 
-def config_line(name: str, steps: int = 100, warmup: int = 10, device: int = 0):
-    """One BASELINE config at full size on this GPU (N = 1 extra key)."""
+def config_line(name: str, steps: int = 1000, warmup: int = 10, device: int = 0):
+    """One BASELINE config at full size on this GPU (N = 1 extra key), timed like the headline
+    (1 000 steps: at 100 the first graph launch's host latency and the final wait were 2-8 % of a
+    config2 / config5 window)."""
     t0 = time.time()
     p = rig.make_config(name)
     gen_s = time.time() - t0
