@@ -245,8 +245,9 @@ def config_line(name: str, steps: int = 1000, warmup: int = 10, device: int = 0)
            "step_distribution": m["dist"],
            "rig_generation_s": round(gen_s, 2)}
     if solve["warm"] or solve["direct"]:
-        # m > 30: solves by refinement with the previous step's inverse (k_sinv, side stream) over
-        # every step of this process (ramp, warmup, timed, window), and how many fell back
+        # solves by refinement with the previous system's inverse (m > 30: k_sinv_helper on a side
+        # stream; m <= 30: the linearisation launch's spare workgroup) over every step of this process
+        # (ramp, warmup, timed, window), and how many fell back
         out["warm_solve"] = solve
     fp = load_profile("fp64", name, p.n_photos)
     if fp and fp.get("fp64_flops_per_launch"):

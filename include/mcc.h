@@ -164,14 +164,19 @@ int mcc_peer_init(mcc_problem *p, const unsigned char *handles /* [64 * nranks],
 int mcc_peer_enable(mcc_problem *p, int on);
 
 /* ---- diagnostics / measurement */
-/* the m > 30 split step's warm solves since mcc_create (k_solve refines with the previous step's
- * inverse, which a resident helper kernel computes while the step linearises): out[5] = {solves by
- * refinement, refinement corrections in them, refinements that did not converge (the direct
- * elimination ran instead), direct solves for want of an inverse (an optimisation's first step, or
- * the previous system was not positive definite), solves that had to wait for the helper}; all zero
- * when the problem takes the direct elimination only (m <= 30, m > 96, MCC_WARM=0).  Which solve a
- * step takes depends on the systems only, never on timing: a step waits for the helper as long as
- * needed, up to MCC_WARM_TIMEOUT_MS (default 10000), after which it fails with MCC_ETIMEOUT. */
+/* the warm solves since mcc_create: out[5] = {solves by refinement with the previous system's inverse,
+ * refinement corrections in them, refinements that did not converge (the direct elimination ran
+ * instead), direct solves for want of an inverse (an optimisation's first step(s), or the previous
+ * system was not positive definite), steps that had to wait for the inverse's producer}.
+ * m > 30 split step: k_solve refines with the inverse a resident helper kernel computes while the step
+ * linearises; it waits for the helper as long as needed, up to MCC_WARM_TIMEOUT_MS (default 10000),
+ * after which the step fails with MCC_ETIMEOUT.  m <= 30 (MCC_SMALL_WARM, default on; single GPU or the
+ * peer transport): a spare workgroup of the step's linearisation launch inverts the previous system,
+ * and the final solve refines with it (the fused step: with the previous launch's, two updates stale);
+ * the last field counts fused steps whose final arriver waited for the spare to acknowledge its inputs,
+ * with the same MCC_WARM_TIMEOUT_MS bound.  All zero when the problem takes the direct elimination only
+ * (m > 96, MCC_WARM=0, MCC_SMALL_WARM=0, RCCL on the fused step).  Which solve a step takes depends on
+ * the systems only, never on timing. */
 int mcc_solve_stats(mcc_problem *p, long long *out);
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
@@ -200,9 +205,10 @@ int mcc_timing_windows(mcc_problem *p, int n_windows, int steps, double *ms_per_
  * (k_group, or k_prep + k_edge + k_photo), `launches` of them in ONE captured graph bracketed by two
  * HIP events on the problem's stream -- the kernels back to back as the step graphs run them, with
  * no event between them (events recorded inside a captured graph carry no timestamps on HIP).  Each
- * launch re-applies the pending photo update, so the parameters are restored after the window; the
- * Schur slots and photo factors then hold a linearisation at those drifted parameters, which the
- * next steps overwrite (a timing probe, not a step).  MCC_EINVAL for a fused-step problem. */
+ * launch re-applies the pending photo update and rewrites its operands (Y', z'), so the parameters and
+ * those operands are restored after the window: the next step continues the trajectory it would have
+ * taken without the probe (the Schur slots and photo sums the probe leaves are outputs the next step
+ * rewrites before reading).  MCC_EINVAL for a fused-step problem. */
 int mcc_timing_linearize(mcc_problem *p, int launches, double *ms_per_launch);
 /* average time (ms) of the step's data-path exchange over the same window, and the exchanges:
  * RCCL all-reduces by HIP event pairs around each ncclAllReduce, the peer transport by the

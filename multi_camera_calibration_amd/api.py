@@ -369,10 +369,11 @@ class BundleAdjuster:
         return dict(corners=v[0].value, edges=v[1].value, photos=v[2].value, alg_bytes=v[3].value)
 
     def solve_stats(self):
-        """The m > 30 warm solves (mcc_solve_stats): solves by refinement with the previous step's
-        inverse, their refinement corrections, refinements that fell back to the direct elimination,
-        direct solves for want of an inverse, solves that waited for the helper (the choice of solve
-        never depends on the wait; all zero on the direct-only paths)."""
+        """The warm solves (mcc_solve_stats; m > 30: the helper kernel's inverse, m <= 30: the spare
+        workgroup's): solves by refinement with the previous system's inverse, their refinement
+        corrections, refinements that fell back to the direct elimination, direct solves for want of an
+        inverse, steps that waited for the inverse's producer (the choice of solve never depends on the
+        wait; all zero on the direct-only paths)."""
         v = (ctypes.c_longlong * 5)()
         _check(lib().mcc_solve_stats(self.h, v), "mcc_solve_stats")
         return dict(warm=v[0], corrections=v[1], fallbacks=v[2], direct=v[3], waited=v[4])

@@ -138,12 +138,37 @@ void host_rodrigues_m2v(const double* Rin, double* r) {
     r[0] = rx; r[1] = ry; r[2] = rz;
 }
 
+// computeTiltProjectionMatrix (OpenCV calib3d, distortion_model.hpp) for the tilted-sensor model of
+// cv::projectPoints with 14 coefficients, which src/mymulticalib.cpp:566 reaches with whatever
+// Distortion the camera XML holds (:118-132): matTilt = matProjZ * (matRotY * matRotX), row-major,
+// Matx products summed left to right from 0
+void tilt_matrix(double tx, double ty, double M[9]) {
+    const double cx = std::cos(tx), sx = std::sin(tx), cy = std::cos(ty), sy = std::sin(ty);
+    const double rx[9] = {1, 0, 0, 0, cx, sx, 0, -sx, cx};
+    const double ry[9] = {cy, 0, -sy, 0, 1, 0, sy, 0, cy};
+    double rxy[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int k = 0; k < 3; ++k) s += ry[3 * i + k] * rx[3 * k + j];
+            rxy[3 * i + j] = s;
+        }
+    const double pz[9] = {rxy[8], 0, -rxy[2], 0, rxy[8], -rxy[5], 0, 0, 1};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int k = 0; k < 3; ++k) s += pz[3 * i + k] * rxy[3 * k + j];
+            M[3 * i + j] = s;
+        }
+}
+
 }  // namespace
 
 struct mcc_problem {
     int model = 0, C = 0, V = 0, E = 0, nd = 0, m = 0, P = 0, device = 0;
     long long corners = 0;
-    bool rational = false, prism = false;
+    bool rational = false;
+    int prism = 0;   // 1: thin prism s1..s4, 2: + the tilted sensor (nd = 14, tau != 0)
     int has_back = 0;
     int max_epp = 1, nblk = 0, n_items = 0, n_pairs = 0, n_norm_chunks = 0;
     size_t n_pair_doubles = 0;   // Schur pair-product slots (36 or 48 doubles each)
@@ -172,6 +197,7 @@ struct mcc_problem {
     DevBuf<long long> stamps;
     DevBuf<double> ds_rt, Y, pairprod, zp, gp_tot, item_out, packed, dg, delta, photo_norm, alpha, contrib, gsum, W;
     DevBuf<double> erec, echain, eh;   // split step (m > 30): per-edge records
+    DevBuf<double> tilt;               // [C][9] matTilt (prism == 2)
     DevBuf<double> ssinv;              // m <= 30 warm solve: the previous system's inverse [m x m]
     DevBuf<int> ssinv_ok;
     DevBuf<int> photo_ptr, photo_corner, edge_gblock, block_items, edge_photo, counter, cnt, cnt_blk;
@@ -200,6 +226,7 @@ struct mcc_problem {
     // it fails with MCC_ETIMEOUT), the helper's idle exit (the wait bound plus the peer timeout: a
     // k_solve may sit in a peer exchange before it publishes), the test delay (MCC_WARM_DELAY_US)
     long long warm_wait_ticks = 1000000000LL, warm_idle_ticks = 4000000000LL, warm_delay_ticks = 0;
+    long long spare_delay_ticks = 0;  // MCC_SPARE_DELAY_US (test): the fused step's spare starts this late
     int fault_photo = -1;            // MCC_FAULT_PHOTO (test): LinArgs::fault_photo
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
@@ -217,7 +244,10 @@ struct mcc_problem {
     // mcc_timing_linearize: a graph of lin_graph_n launches of the split step's linearisation kernels
     hipGraphExec_t lin_graph = nullptr;
     int lin_graph_n = 0;
-    DevBuf<float> xsave;   // x across that window (each launch applies the pending photo update again)
+    // x, and the pending photo update's operands Y' and z', across that window: each launch applies the
+    // pending update again and rewrites Y' and z' at the drifted parameters
+    DevBuf<float> xsave;
+    DevBuf<double> ysave, zpsave;
     int graph_sizes = kGraphSizes;   // MCC_GRAPH_SIZES (A/B of the launch granularity)
     bool use_graph = true;
     // the device State is in free-running mode (crit_type 0) since the last mcc_step: later
@@ -259,7 +289,9 @@ struct mcc_problem {
 namespace {
 
 mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
-    return mcc::SolveCtx{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+    mcc::SolveCtx c{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
+    c.sstats = p->ssinv.p ? p->warm_stats.p : nullptr;   // the m <= 30 warm solve's statistics
+    return c;
 }
 
 mcc::WarmCtx warm_ctx(mcc_problem* p) {
@@ -320,7 +352,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
     la.obj_x = p->obj_x.p; la.obj_y = p->obj_y.p; la.obj_z = p->obj_z.p;
     la.img_u = p->img_u.p; la.img_v = p->img_v.p;
     la.x = p->x.p;
-    la.K = p->K.p; la.D = p->D.p; la.xi = p->xi.p;
+    la.K = p->K.p; la.D = p->D.p; la.xi = p->xi.p; la.tilt = p->tilt.p;
     la.cam_rt = p->cam_rt.p; la.ds_rt = p->ds_rt.p;
     la.nd = p->nd; la.global_dim = p->m;
     la.n_cams = p->C; la.has_back = p->has_back;
@@ -338,6 +370,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
     la.fault_photo = p->fault_photo;
     la.ssinv = swarm ? p->ssinv.p : nullptr;
     la.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
+    la.spare_wait = p->warm_wait_ticks;
+    la.spare_delay = p->spare_delay_ticks;
     // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
     // split path: the packed system is summed by RCCL and solved by k_solve.  The peer transport
     // keeps one kernel per step: the final arriver exchanges with the peers and solves.
@@ -526,6 +560,8 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     p->h_state->max_count = max_count;
     p->h_state->eps = eps;
     p->h_state->error = 0;
+    // the fused step's spare protocol restarts (the stream is idle: no spare of an earlier launch runs)
+    p->h_state->spare_seq = p->h_state->spare_ack = 0;
     HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     return MCC_OK;
 }
@@ -598,9 +634,6 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             return fail(MCC_EINVAL, "BACK edge without doubleSideTransform (the reference dereferences an empty Mat)");
         if (side == MCC_BACK && d->model == MCC_MODEL_OMNI) return fail(MCC_EINVAL, "BACK edges are pinhole only");
     }
-    for (int c = 0; c < C && d->model != MCC_MODEL_OMNI; ++c)
-        if (d->nd == 14 && (d->D[14 * c + 12] != 0.f || d->D[14 * c + 13] != 0.f))
-            return fail(MCC_EINVAL, "tilted-sensor distortion (tau_x, tau_y != 0) is not supported");
 
     mcc_problem* p = new mcc_problem();
     p->model = d->model; p->C = C; p->V = V; p->E = E; p->nd = d->nd; p->device = d->device;
@@ -625,8 +658,24 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         for (int c = 0; c < C; ++c)
             for (int q = 5; q < std::min(d->nd, 12); ++q) {
                 const float v = d->D[d->nd * c + q];
-                if (v != 0.f) (q < 8 ? p->rational : p->prism) = true;
+                if (v != 0.f) {
+                    if (q < 8) p->rational = true;
+                    else p->prism = 1;
+                }
             }
+        // the tilted sensor (tau_x, tau_y: D[12], D[13] of 14): matTilt per camera in FP64, as
+        // cvProjectPoints2Internal forms it from the CV_32F coefficients (identity where tau = 0, which
+        // the projection then applies exactly: vecTilt = (xd0, yd0, 1), invProj = 1)
+        bool tilt = false;
+        for (int c = 0; c < C && d->nd == 14; ++c)
+            tilt = tilt || d->D[14 * c + 12] != 0.f || d->D[14 * c + 13] != 0.f;
+        if (tilt) {
+            p->rational = true;   // zero k4..k6 / s1..s4 are exact no-ops in the 14-term formula
+            p->prism = 2;
+            std::vector<double> mt(9 * (size_t)C);
+            for (int c = 0; c < C; ++c) tilt_matrix(d->D[14 * c + 12], d->D[14 * c + 13], mt.data() + 9 * c);
+            HIPC(p->tilt.upload(mt.data(), mt.size()));
+        }
     }
 
     // ---- photo-major edge order (stable within a photo: reference edge order)
@@ -680,7 +729,9 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     int n_cu = 256;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
-    const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64;
+    // (the tilted sensor takes the split step: the fused kernel's PRISM variants already hold 256 VGPRs,
+    // and the tilt's per-corner 3 x 3 map and 2 x 2 chain spill there; k_group / k_edge have room)
+    const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64 && p->prism != 2;
     p->fused = fusable && V <= 2 * n_cu;
     if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
     if (!p->fused && p->max_epp > 64)
@@ -976,6 +1027,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             HIPC(p->ssinv.alloc(2 * (size_t)p->m * p->m));
             HIPC(p->ssinv_ok.alloc(2));
             HIPC(hipMemset(p->ssinv_ok.p, 0, 2 * sizeof(int)));
+            HIPC(p->warm_stats.alloc(5));   // mcc_solve_stats
+            HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
         }
     }
     p->warm = !p->fused && p->m > 30;
@@ -983,6 +1036,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
     if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
     if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
+    if (const char* f = std::getenv("MCC_SPARE_DELAY_US")) p->spare_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
     if (const char* f = std::getenv("MCC_FAULT_PHOTO")) p->fault_photo = std::atoi(f);
     {
         double peer_ms = 30000.0;   // the helper outlives a k_solve's longest wait at a peer exchange
@@ -997,7 +1051,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         HIPC(hipExtMallocWithFlags((void**)&p->prev2, 2 * (size_t)p->prev_stride * sizeof(double), hipDeviceMallocUncached));
         HIPC(hipExtMallocWithFlags((void**)&p->wsync, 4 * sizeof(unsigned), hipDeviceMallocUncached));
         HIPC(hipMemset(p->wsync, 0, 4 * sizeof(unsigned)));
-        HIPC(p->warm_stats.alloc(5));
+        if (!p->warm_stats.p) HIPC(p->warm_stats.alloc(5));
         HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
         HIPC(stream_pool().take(d->device, &p->side, true));
     }
@@ -1017,7 +1071,7 @@ void mcc_destroy(mcc_problem* p) {
     if (p->wsync) (void)hipFree(p->wsync);
     p->warm_stats.release();
     drop_graphs(p);
-    p->xsave.release();
+    p->xsave.release(); p->ysave.release(); p->zpsave.release();
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
     for (auto e : p->ev_x) (void)hipEventDestroy(e);
@@ -1033,7 +1087,7 @@ void mcc_destroy(mcc_problem* p) {
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->corner_err.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
-    p->erec.release(); p->echain.release(); p->eh.release(); p->ssinv.release(); p->ssinv_ok.release();
+    p->erec.release(); p->echain.release(); p->eh.release(); p->tilt.release(); p->ssinv.release(); p->ssinv_ok.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
@@ -1156,7 +1210,7 @@ int mcc_project_error_detail(mcc_problem* p, const float* x, float* edge_err, fl
     HIPCHK(hipMemcpy(p->xerr.p, x, sizeof(float) * p->P, hipMemcpyHostToDevice));
     if (corner_err && !p->corner_err.p) HIPCHK(p->corner_err.alloc(std::max<long long>(p->corners, 1)));
     mcc::ErrArgs a{p->edge_info.p, p->edge_photo.p, p->obj_x.p, p->obj_y.p, p->obj_z.p, p->img_u.p, p->img_v.p,
-                   p->xerr.p, p->K.p, p->D.p, p->xi.p, p->cam_pose.p, p->edge_sum.p,
+                   p->xerr.p, p->K.p, p->D.p, p->xi.p, p->tilt.p, p->cam_pose.p, p->edge_sum.p,
                    corner_err ? p->corner_err.p : nullptr, p->nd, p->m};
     if (p->E) HIPCHK(mcc_launch_project_error(a, p->model, p->E, p->rational, p->prism, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
@@ -1242,9 +1296,9 @@ int mcc_solve_stats(mcc_problem* p, long long* out) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     std::memset(out, 0, 5 * sizeof(long long));
-    if (!p->warm) return MCC_OK;
+    if (!p->warm_stats.p) return MCC_OK;
     HIPCHK(hipStreamSynchronize(p->stream));
-    HIPCHK(hipStreamSynchronize(p->side));
+    if (p->side) HIPCHK(hipStreamSynchronize(p->side));
     HIPCHK(hipMemcpy(out, p->warm_stats.p, 5 * sizeof(long long), hipMemcpyDeviceToHost));
     return MCC_OK;
 }
@@ -1417,12 +1471,20 @@ int mcc_timing_linearize(mcc_problem* p, int launches, double* ms_per_launch) {
         HIPCHK(hipEventCreate(&p->ev_win[1]));
     }
     if (!p->xsave.p) HIPCHK(p->xsave.alloc(p->P));
+    if (!p->ysave.p) HIPCHK(p->ysave.alloc(p->Y.n));
+    if (!p->zpsave.p) HIPCHK(p->zpsave.alloc(p->zp.n));
     HIPCHK(hipMemcpyAsync(p->xsave.p, p->x.p, sizeof(float) * p->P, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(p->ysave.p, p->Y.p, sizeof(double) * p->Y.n, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(p->zpsave.p, p->zp.p, sizeof(double) * p->zp.n, hipMemcpyDeviceToDevice, p->stream));
     HIPCHK(hipEventRecord(p->ev_win[0], p->stream));
     HIPCHK(hipGraphLaunch(p->lin_graph, p->stream));
     HIPCHK(hipEventRecord(p->ev_win[1], p->stream));
-    // the parameters as before the window (each launch re-applied the pending photo update)
+    // the parameters and the pending update's operands as before the window (each launch re-applied
+    // the pending photo update and rewrote Y', z'), so the next step continues the trajectory; the
+    // state (pending, alpha, dg) is untouched by the linearisation kernels
     HIPCHK(hipMemcpyAsync(p->x.p, p->xsave.p, sizeof(float) * p->P, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(p->Y.p, p->ysave.p, sizeof(double) * p->Y.n, hipMemcpyDeviceToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(p->zp.p, p->zpsave.p, sizeof(double) * p->zp.n, hipMemcpyDeviceToDevice, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, p->ev_win[0], p->ev_win[1]));

@@ -294,7 +294,7 @@ __device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, i
 #ifndef MCC_GROUP_OCC
 #define MCC_GROUP_OCC 2   // k_group workgroups per CU the register budget allows (LDS: ~64 KB each)
 #endif
-template <int MODEL, bool RATIONAL, bool PRISM, bool BACK, int L>
+template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
 __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_group(LinArgs a) {
     constexpr int NT = kGroupRound * L, EPW = 64 / L;   // threads; edges per wave
     static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
         extern __shared__ __attribute__((aligned(16))) double smem_spare[];
-        if (!st->done) small_inverse(a, smem_spare);
+        small_inverse(a, smem_spare, false);
         return;
     }
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
@@ -404,13 +404,16 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
 #pragma unroll
                 for (int k = 0; k < 3; ++k) { om2[k] = a.x[6 * (c - 1) + k]; T2[k] = a.x[6 * (c - 1) + 3 + k]; }
             }
-            double* kt = ktab + 20 * c;
+            double* kt = ktab + kGIntr * c;
             const float* Kc = a.K + 9 * c;
             kt[0] = Kc[0]; kt[1] = Kc[4]; kt[2] = Kc[2]; kt[3] = Kc[5]; kt[4] = Kc[1];
             kt[5] = MODEL == MCC_MODEL_OMNI ? (double)a.xi[c] : 0.0;
             const int nd = a.nd;
 #pragma unroll
             for (int q = 0; q < 12; ++q) kt[6 + q] = q < nd ? (double)a.D[nd * c + q] : 0.0;
+            if (PRISM == 2)
+#pragma unroll
+                for (int q = 0; q < 9; ++q) kt[18 + q] = a.tilt[9 * c + q];
         } else if (BACK && tid == DST) {   // the double-side transform (BACK edges; DoubleSide's global block)
             if (MODEL == MCC_MODEL_DOUBLESIDE) {
 #pragma unroll
@@ -533,13 +536,13 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
         const bool ev = le < gne;
         const int4 info = ev ? sInfo[le] : make_int4(0, 0, 0, 0);
         const int cam = info.x;
-        double* P = sP + 32 * es;
+        double* P = sP + kGRecP * es;
         double* Gbe = sGb + 56 * es;
         if (rb > 0 && ev) stage(info.z, 0, min(info.w, kGChunk));
         if (ev) {
             group_prologue<MODEL, BACK, L>(sph + 24 * seq[le], ctab + 24 * cam, sds, info.y, sub, rec + kGRec * le, P, Gbe);
-            const double* kt = ktab + 20 * cam;
-            for (int k = sub; k < 18; k += L) P[12 + k] = kt[k];
+            const double* kt = ktab + kGIntr * cam;
+            for (int k = sub; k < (PRISM == 2 ? 27 : 18); k += L) P[12 + k] = kt[k];
         }
         wave_sync_lds();
         if (rb == 0) SSTAMP(stp, 3, 0);
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
                 if (MODEL == MCC_MODEL_OMNI)
                     omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
                 else
-                    pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
+                    pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D, Pq + 30);
                 const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
                 if (a.resid) {
                     const size_t c = (size_t)info.z + cc0 + i;

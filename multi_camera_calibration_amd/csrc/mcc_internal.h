@@ -24,12 +24,18 @@ struct State {
     int pending;      // a solved photo update waits to be applied by the next k_linearize
     unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
     long long xchg_ticks; // s_memrealtime ticks (100 MHz) inside peer exchanges, summed (monotonic)
+    // the fused step's m <= 30 warm solve (k_linearize's spare workgroup, small_inverse): fused launches
+    // since set_state (the final arriver advances it), and the spare's acknowledgement -- spare_seq + 1
+    // once it holds this launch's inputs (state words, the packed system) in LDS.  The final arriver
+    // writes neither the packed system nor the state before it has seen that acknowledgement.
+    unsigned int spare_seq, spare_ack;
 };
 // State::error bits
 constexpr int kErrPhotoNotPD = 1;    // a photo's 6 x 6 block (any rank: summed through the exchange)
 constexpr int kErrCameraNotPD = 2;   // the reduced camera system
 constexpr int kErrPeerTimeout = 4;   // a peer did not deliver its system
-constexpr int kErrWarmTimeout = 8;   // the warm-solve helper did not deliver the previous inverse
+constexpr int kErrWarmTimeout = 8;   // the warm-solve helper did not deliver the previous inverse, or
+                                     // the fused step's spare did not acknowledge its inputs
 
 // Peer transport (multi-GPU without RCCL in the step): every rank's final arriver writes its packed
 // reduced system straight into every peer's inbox over xGMI, then sums all ranks' systems in rank
@@ -53,6 +59,10 @@ struct SolveCtx {
     double* delta;    // [P]
     int m, do_update;
     long long* stamps;   // MCC_DIAG: solve phase stamps (set by k_schur's last arriver)
+    // m <= 30 warm solve statistics (mcc_solve_stats, the m > 30 helper's layout): refinements tried,
+    // corrections, refinements that fell back to the elimination, eliminations without an inverse,
+    // fused steps whose final arriver waited for the spare's acknowledgement (null: off)
+    long long* sstats;
 };
 
 struct LinArgs {
@@ -65,6 +75,7 @@ struct LinArgs {
     const float* img_u; const float* img_v;
     float* x;                 // [P] float32 parameters [global m | photos] (photo part updated in place)
     const float* K; const float* D; const float* xi;
+    const double* tilt;       // [C][9] the tilted-sensor matTilt (nd = 14, tau != 0; null otherwise)
     const float* cam_rt;      // DOUBLESIDE fixed cameras (rvec, tvec) [6C]
     const double* ds_rt;      // PINHOLE doubleSideTransform (rvec, tvec) [6]
     int nd, global_dim, n_cams, has_back;
@@ -116,6 +127,9 @@ struct LinArgs {
     // m <= 30 warm solve: k_group's spare workgroup inverts the previous step's packed system
     double* ssinv;           // [2][m x m] by iteration parity (null: off)
     int* ssinv_ok;           // [2] the iteration + 1 whose spare workgroup formed the buffer (0: none)
+    // the fused step's spare: its wait bound at the final arriver (s_memrealtime ticks; past it the
+    // step fails with kErrWarmTimeout), and a test delay before it reads anything (MCC_SPARE_DELAY_US)
+    long long spare_wait, spare_delay;
 };
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
@@ -134,6 +148,8 @@ __host__ __device__ inline size_t photo_lds_bytes(int gne, int npairs, int ncon)
 
 // k_group (mcc_group.hpp): the fused split step's per-group LDS
 constexpr int kGChunk = 96;       // corners of one edge staged in LDS at a time
+constexpr int kGIntr = 28;        // k_group's LDS intrinsics row: fx fy cx cy skew xi k[12] matTilt[9] pad
+constexpr int kGRecP = 40;        // k_group's per-edge sweep record: R 9 | T 3 | 6 intrinsics | k[12] | matTilt[9] | pad
 constexpr int kGRec = 92;         // doubles per group edge: sE (64: Hgg upper 21 | pad | U 36 | gg 6)
                                   // + Hpp upper 21 | gp 6 | pad; the edge's prologue scratch meanwhile
 
@@ -153,10 +169,10 @@ __host__ __device__ inline GroupLayout group_layout(int gne, int C, int nq, int 
     L.spart = L.sxn + 16 * kPhotoGroup;         // [gne][6] Y'_e^T dg partials of the photo update
     L.sdg = L.spart + 6 * gne;                  // [128] the previous solve's global-block delta
     L.ctab = L.sdg + 128;                       // [C][24] camera R | Jl | T
-    L.ktab = L.ctab + 24 * C;                   // [C][20] fx fy cx cy skew xi k[12]
-    L.sds = L.ktab + 20 * C;                    // [32] double-side transform Rds | Jrds | dst
-    L.sP = L.sds + 32;                          // [16][32] sweep record: R | T | fx fy cx cy skew xi | k[12]
-    L.sGb = L.sP + 32 * kGroupRound;            // [16][56] chain-map blocks [photo 27 | pad | global 27 | pad]
+    L.ktab = L.ctab + 24 * C;                   // [C][kGIntr] fx fy cx cy skew xi k[12] matTilt[9]
+    L.sds = L.ktab + kGIntr * C;                // [32] double-side transform Rds | Jrds | dst
+    L.sP = L.sds + 32;                          // [16][kGRecP] sweep record: R | T | fx fy cx cy skew xi | k[12] | matTilt[9]
+    L.sGb = L.sP + kGRecP * kGroupRound;        // [16][56] chain-map blocks [photo 27 | pad | global 27 | pad]
     L.sU = L.sGb + 56 * kGroupRound;            // per wave: corners [5][96][4] floats | chain {A 36, B 8, X 96} x 4
     L.ndoubles = L.sU + 4 * (5 * kGChunk * 4 / 2);
     L.ndoubles = (L.ndoubles + 1) & ~1;         // 16-B aligned int4 area
@@ -306,6 +322,7 @@ struct ErrArgs {
     const float* img_u; const float* img_v;
     const float* x;
     const float* K; const float* D; const float* xi;
+    const double* tilt;      // [C][9] matTilt (null: no tilt)
     const float* cam_pose;   // DOUBLESIDE [16C]
     float* edge_sum;         // [E] device order
     float* corner_err;       // optional [corners] device order: each corner's float32 L2 error
@@ -318,11 +335,11 @@ struct ErrArgs {
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp);
 size_t mcc_solve_shmem(int m);
 hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, size_t photo_shmem, size_t group_shmem);
-hipError_t mcc_launch_group(const mcc::LinArgs& a, int model, bool rational, bool prism, int lanes,
+hipError_t mcc_launch_group(const mcc::LinArgs& a, int model, bool rational, int prism, int lanes,
                             size_t group_shmem, hipStream_t s);
-hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
+hipError_t mcc_launch_split(const mcc::LinArgs& a, int model, bool rational, int prism, size_t photo_shmem,
                             hipStream_t s);
-hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s);
+hipError_t mcc_launch_linearize(const mcc::LinArgs& a, int model, int n_photos, int max_epp, bool rational, int prism, hipStream_t s);
 hipError_t mcc_launch_schur(const mcc::SchurArgs& a, int grid, hipStream_t s);
 hipError_t mcc_launch_solve(const mcc::SolveArgs& a, hipStream_t s);
 hipError_t mcc_launch_peer_push(const mcc::PeerCtx& pc, const mcc::State* st, const double* vals, hipStream_t s);
@@ -332,4 +349,4 @@ hipError_t mcc_launch_backsub(const mcc::BacksubArgs& a, hipStream_t s);
 hipError_t mcc_launch_delay(long long ticks, hipStream_t s);
 hipError_t mcc_launch_peer_handshake(const mcc::PeerCtx& pc, mcc::State* st, double* out, hipStream_t s);
 hipError_t mcc_launch_peer_max(const mcc::PeerCtx& pc, mcc::State* st, double* v, hipStream_t s);
-hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s);
+hipError_t mcc_launch_project_error(const mcc::ErrArgs& a, int model, int n_edges, bool rational, int prism, hipStream_t s);

@@ -236,7 +236,9 @@ struct PhotoLds {
     double dgl[128];     // global-block delta of the previous solve (pending update)
     double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
     double cn[2];        // state snapshot: camera-block ||G||^2, ||x||^2 of the last update
-    int iter0, pad1[3];  // state snapshot: completed updates
+    int iter0;           // state snapshot: completed updates
+    unsigned seq0;       // state snapshot: State::spare_seq (the fused step's spare acknowledgement)
+    int pad1[2];
     int bn[8];           // per camera block: number of the photo's edges in it (fused step)
     unsigned char bl[5][64];   // per camera block: those edges in edge order
     // followed by the camera table [C][kCamStride], the intrinsics [C][kIntrStride] and the
@@ -580,12 +582,17 @@ __device__ __forceinline__ void edge_prologue_wave(const PhotoLds& P, const doub
 
 // ---------------------------------------------------------------- per-corner models
 // Pinhole (cvProjectPoints2Internal order).  Float32 pixel and D = d(u,v)/dXc (2x3).
-template <bool RATIONAL, bool PRISM>
+// PRISM: 0 k1..k6 (RATIONAL: k4..k6), 1 + thin prism s1..s4, 2 + the tilted sensor (tau_x, tau_y):
+// tm = matTilt (3 x 3, row-major; computeTiltProjectionMatrix, formed on the host in FP64 --
+// mcc_create), vecTilt = matTilt (xd0, yd0, 1), (xd, yd) = vecTilt(0..1) / vecTilt(2), and the 2 x 2
+// dMatTilt = (matTilt(r, c) vecTilt(2) - matTilt(2, c) vecTilt(r)) / vecTilt(2)^2 in the chain
+template <bool RATIONAL, int PRISM>
 __device__ __forceinline__ void pinhole_corner(const double* R, const double* T, const double* k,
                                                double fx, double fy, double cx, double cy,
                                                double X, double Y, double Z, double* Yr,
-                                               float& u, float& v, double* D) {
+                                               float& u, float& v, double* D, const double* tm = nullptr) {
     double x, y, z, r2, r4, r6, cdist, icdist2;
+    double t0 = 0.0, t1 = 0.0, t2 = 1.0, ip = 1.0;   // vecTilt, invProj (PRISM == 2)
     {
 #pragma clang fp contract(off)
         Yr[0] = R[0] * X + R[1] * Y + R[2] * Z;
@@ -609,6 +616,14 @@ __device__ __forceinline__ void pinhole_corner(const double* R, const double* T,
             xd = xd + k[8] * r2 + k[9] * r4;
             yd = yd + k[10] * r2 + k[11] * r4;
         }
+        if (PRISM == 2) {   // matTilt * Vec3d(xd0, yd0, 1): Matx's row sums, left to right
+            t0 = tm[0] * xd + tm[1] * yd + tm[2];
+            t1 = tm[3] * xd + tm[4] * yd + tm[5];
+            t2 = tm[6] * xd + tm[7] * yd + tm[8];
+            ip = t2 ? 1. / t2 : 1;
+            xd = ip * t0;
+            yd = ip * t1;
+        }
         u = (float)(xd * fx + cx);
         v = (float)(yd * fy + cy);
     }
@@ -620,10 +635,18 @@ __device__ __forceinline__ void pinhole_corner(const double* R, const double* T,
     double P1 = 0.0, P2 = 0.0;
     if (PRISM) { P1 = k[8] + 2 * r2 * k[9]; P2 = k[10] + 2 * r2 * k[11]; }
     const double xy2g = 2 * x * y * g;
-    const double m00 = cc + 2 * x * x * g + 2 * k[2] * y + 6 * k[3] * x + 2 * x * P1;
-    const double m01 = xy2g + 2 * k[2] * x + 2 * k[3] * y + 2 * y * P1;
-    const double m10 = xy2g + 2 * k[2] * x + 2 * k[3] * y + 2 * x * P2;
-    const double m11 = cc + 2 * y * y * g + 6 * k[2] * y + 2 * k[3] * x + 2 * y * P2;
+    double m00 = cc + 2 * x * x * g + 2 * k[2] * y + 6 * k[3] * x + 2 * x * P1;
+    double m01 = xy2g + 2 * k[2] * x + 2 * k[3] * y + 2 * y * P1;
+    double m10 = xy2g + 2 * k[2] * x + 2 * k[3] * y + 2 * x * P2;
+    double m11 = cc + 2 * y * y * g + 6 * k[2] * y + 2 * k[3] * x + 2 * y * P2;
+    if (PRISM == 2) {   // the tilt's 2 x 2 Jacobian (dMatTilt) after the distortion map
+        const double ip2 = ip * ip;
+        const double d00 = (tm[0] * t2 - tm[6] * t0) * ip2, d01 = (tm[1] * t2 - tm[7] * t0) * ip2;
+        const double d10 = (tm[3] * t2 - tm[6] * t1) * ip2, d11 = (tm[4] * t2 - tm[7] * t1) * ip2;
+        const double n00 = d00 * m00 + d01 * m10, n01 = d00 * m01 + d01 * m11;
+        const double n10 = d10 * m00 + d11 * m10, n11 = d10 * m01 + d11 * m11;
+        m00 = n00; m01 = n01; m10 = n10; m11 = n11;
+    }
     const double fzx = fx * z, fzy = fy * z;
     D[0] = fzx * m00;
     D[1] = fzx * m01;
@@ -914,19 +937,50 @@ __device__ __forceinline__ double photo_flag_norm(int err, int w, double v) {
 template <bool LARGE>
 __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, double* r, double normG2, double normX2,
                                              const WarmCtx* warm = nullptr, const double* Iv = nullptr);
-__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A);
+
+__device__ __forceinline__ unsigned ld_agent_u32(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The fused step's final arriver, each thread before its first write of the packed system: the
+// spare's acknowledgement (ack, loaded with the thread's batch) must be this launch's (want = the
+// spare_seq every workgroup of the launch read + 1).  Polls (sc1 loads) up to LinArgs::spare_wait; the
+// spare is the grid's last workgroup and the other photos have exited, so it runs unless the device is
+// held by others.  false: gave up (*to = 1; the step fails at the next barrier, spare_failed).
+__device__ __forceinline__ bool spare_wait(const LinArgs& a, unsigned ack, unsigned want, int* to, int* waited) {
+    if (ack == want) return true;
+    *waited = 1;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    do {
+        __builtin_amdgcn_s_sleep(2);
+        if (ld_agent_u32(&a.state->spare_ack) == want) return true;
+    } while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < a.spare_wait);
+    *to = 1;
+    return false;
+}
+// after a barrier behind every thread's spare_wait: the spare never acknowledged -> fail the step
+// (MCC_ETIMEOUT), stop the loop; nothing of the step was written
+__device__ __forceinline__ bool spare_failed(State* st, int ack_to) {
+    if (!ack_to) return false;
+    if (threadIdx.x == 0) {
+        atomicOr(&st->error, kErrWarmTimeout);
+        st->done = 1;
+    }
+    return true;
+}
+__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool ack);
 
 // ---------------------------------------------------------------- k_linearize
 // Diagnostic builds (-DMCC_DIAG, libmcc_diag.so only) stamp s_memtime at phase boundaries.
 // The m <= 30 single-kernel step (a.fused); m > 30 takes the split step below.
-template <int MODEL, bool RATIONAL, bool PRISM>
+template <int MODEL, bool RATIONAL, int PRISM>
 __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
+    static_assert(PRISM != 2, "the tilted sensor takes the split step (mcc_create)");
     State* st = a.state;
     const int photo = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     if (photo == a.n_photos) {   // the spare workgroup (a.ssinv): the previous system's inverse
-        if (!st->done) small_inverse(a, smem);
+        small_inverse(a, smem, true);
         return;
     }
     // ---- round trip 1: everything indexed by the photo alone
@@ -964,6 +1018,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
         else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
         else if (lane == 10) P.iter0 = st->iter;
+        else if (lane == 11) P.seq0 = st->spare_seq;
         if (pending) {
             if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
@@ -1373,6 +1428,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     __shared__ double nrm2[2];
     const int iter0 = P.iter0;   // read before S overwrites the photo record
     const double cnG = P.cn[0], cnX = P.cn[1];
+    // the spare's acknowledgement of this launch (small_inverse): no thread writes the packed system or
+    // the state before it has seen it; a thread that gave up (spare_wait's bound) sets ack_to, and the
+    // step then fails after the next barrier instead of solving
+    const bool spare = a.ssinv != nullptr;
+    const unsigned want = P.seq0 + 1u;
+    __shared__ int ack_to, ack_waited;
+    if (tid == 0) ack_to = ack_waited = 0;
     __syncthreads();
     auto place = [&](int t, double v) {
         if (t < ntri) {
@@ -1421,20 +1483,29 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
         for (int q = 0; q < 24; ++q) b[q] = ld_sc1(a.gsum + (size_t)min(q, ng - 1) * Lcp + tt);
         // the error word after the sums' loads: the compiler makes it uniform (v_readfirstlane) and
-        // waits for it at once, which in front of the batch would be a memory round trip of its own
+        // waits for it at once, which in front of the batch would be a memory round trip of its own;
+        // the spare's acknowledgement likewise (normally long there: the spare reads its inputs first)
         const int err_now = photo_error(st);
+        const unsigned ack = spare ? ld_agent_u32(&st->spare_ack) : want;
         double v = 0.0;
 #pragma unroll
         for (int q = 0; q < 24; ++q) v += q < ng ? b[q] : 0.0;   // group order (sum_sc1's additions)
-        if (tid < Lc) finish_entry(tid, v, err_now);
-    } else {
+        if (spare_wait(a, ack, want, &ack_to, &ack_waited) && tid < Lc) finish_entry(tid, v, err_now);
+    } else if (spare_wait(a, spare ? ld_agent_u32(&st->spare_ack) : want, want, &ack_to, &ack_waited)) {
         for (int t = tid; t < Lc; t += blockDim.x) {
             const double v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
             finish_entry(t, v, photo_error(st));
         }
     }
+    // (thread 0 has seen the acknowledgement: the spare read spare_seq before it; the next launch's
+    // photos and spare read the new value)
+    if (spare && tid == 0 && !ack_to) st->spare_seq = want;
     STAMP(17);   // thread 0's share of the assembly done (MCC_DIAG)
     if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
+        if (spare) {
+            __syncthreads();
+            if (spare_failed(st, ack_to)) { RSTAMP(15); return; }
+        }
         if (!peer_exchange(a.peer, st, a.packed)) { RSTAMP(15); return; }
         for (int t = tid; t < Lc; t += blockDim.x) place(t, a.packed[t]);
     }
@@ -1450,6 +1521,8 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         if (tid == 0) iv_ok = ivtag == iter0;
     }
     __syncthreads();
+    if (spare && spare_failed(st, ack_to)) { RSTAMP(15); return; }
+    if (spare && tid == 0 && ack_waited && a.solve.sstats) atomicAdd((unsigned long long*)(a.solve.sstats + 4), 1ull);
     STAMP(12);
     SolveCtx sc = a.solve;
 #ifdef MCC_DIAG
@@ -1864,7 +1937,7 @@ constexpr int kEdgeChunk = 96;    // corners of one edge staged in LDS at a time
 // L = 8 sweeps an 88-corner edge in 11 full rounds (16 lanes: 5.5), halves the butterfly per
 // edge, and stages corners in 48-corner chunks; the chain then runs in passes of 4 edges with 16
 // lanes each (edge_chain_xh) so that its LDS fits in the corner area.
-template <int MODEL, bool RATIONAL, bool PRISM, int L>
+template <int MODEL, bool RATIONAL, int PRISM, int L>
 __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) ? 3 : MCC_EDGE_WAVES) void k_edge(LinArgs a) {
     static_assert(L == 16 || L == 8, "k_edge: 16 or 8 lanes per edge");
     if (a.state->done) return;
@@ -1879,7 +1952,7 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
     // (A', b', the chain maps' nonzero blocks, X = A' G), and the edge's pose / camera (8.6 KB: 4
     // waves per SIMD)
     __shared__ __attribute__((aligned(16))) union { float C[5][CHK][GPB]; EdgeChain H[4]; } sU;
-    __shared__ double sP[GPB][30];
+    __shared__ double sP[GPB][PRISM == 2 ? 40 : 30];   // + matTilt (the tilted sensor)
     __shared__ int sI[GPB][2];   // corner offset and count, re-read per chunk (nothing stays live through the sweep)
     auto& sC = sU.C;
     // a workgroup's edges past the last are swept as empty (no early exit: the chain passes map
@@ -1928,9 +2001,10 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
         const double* er = a.erec + 12 * (size_t)(ev ? e : 0);
         const float* Kc = a.K + 9 * cam;
         const int nd = a.nd;
-        for (int t = sub; t < 30; t += L) {
+        for (int t = sub; t < (PRISM == 2 ? 39 : 30); t += L) {
             double v;
-            if (t < 12) v = er[t];
+            if (t >= 30) v = a.tilt[9 * cam + (t - 30)];
+            else if (t < 12) v = er[t];
             else if (t < 17) v = (double)Kc[t == 12 ? 0 : t == 13 ? 4 : t == 14 ? 2 : t == 15 ? 5 : 1];
             else if (t == 17) v = MODEL == MCC_MODEL_OMNI ? (double)a.xi[cam] : 0.0;
             else v = t - 18 < nd ? (double)a.D[nd * cam + (t - 18)] : 0.0;
@@ -1970,7 +2044,7 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
             if (MODEL == MCC_MODEL_OMNI)
                 omni_corner(R, T, kd, fx, fy, cx, cy, sk, xi, X, Y, Z, Yr, u, v, D);
             else
-                pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D);
+                pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, X, Y, Z, Yr, u, v, D, P + 30);
             const float euf = ou - u, evf = ov - v;   // fl32(imagePoints - imagePoints2)
             if (a.resid) {
                 const size_t c = (size_t)off + c0 + i;
@@ -3138,26 +3212,42 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 // chain of broadcasts (~5.4 k cycles).  The inverse is formed OFF the critical
 // path: k_group launches one spare workgroup beyond its groups (250 groups on 256 CUs at config4), which
 // inverts the packed system the previous step's k_schur left (gj_inverse_rows) while the groups
-// linearise; k_schur's final arriver reads it after the kernel boundary.  Every step forms it, so the
-// branch a step takes -- refinement, or the elimination when there is no previous system (an
-// optimisation's first step, a linearisation-only step) or the refinement does not converge -- is a
-// function of the systems alone, never of timing.
+// linearise; k_schur's final arriver reads it after the kernel boundary.  The fused step (k_linearize)
+// appends the spare to the same launch whose final arriver rewrites the packed system and the state, so
+// there the spare acknowledges (State::spare_ack = spare_seq + 1) once it holds its inputs in LDS, and
+// the final arriver writes neither before it has seen that (spare_wait): the spare always inverts the
+// previous launch's system and tags it with this launch's iteration, however late it is scheduled.
+// Every step forms it, so the branch a step takes -- refinement, or the elimination when there is no
+// previous system (an optimisation's first step, a linearisation-only step) or the refinement does not
+// converge -- is a function of the systems alone, never of timing.
 
 // Gauss-Jordan on [S | I] in LDS by the whole workgroup (S from the packed upper triangle in global
 // memory; thread-per-element updates, two barriers per pivot: ~2 us at m = 18, off the critical path,
 // and no register arrays that would raise k_group's register pressure); Sinv row i = (E row i) / d_i.
-// ok = 0 when a pivot is not > 0.
-__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
-    const State* st = a.state;
+// ok = 0 when a pivot is not > 0.  ack: the fused step's spare (above).
+__device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool ack) {
+    State* st = a.state;
     const int tid = threadIdx.x, nt = blockDim.x, m = a.global_dim, W = 2 * m;
+    if (ack && a.spare_delay > 0) {   // test (MCC_SPARE_DELAY_US): a spare scheduled late
+        if (tid == 0) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < a.spare_delay) __builtin_amdgcn_s_sleep(8);
+        }
+        __syncthreads();
+    }
     // buffer iteration & 1, tagged iteration + 1 (0: none): k_schur of this step reads it, the fused
     // step's final arriver of the NEXT launch does (this launch's is still inverting)
-    const int it = st->iter, pend = st->pending;
+    const int done = st->done, it = st->iter, pend = st->pending;
+    const unsigned seq = st->spare_seq;
+    if (done) return;   // no final arriver waits (the photos see the same word)
     double* out = a.ssinv + (size_t)(it & 1) * m * m;
     int* okp = a.ssinv_ok + (it & 1);
     __shared__ int ok_s;
     if (!pend) {   // no update step before this one: no system to precondition with
-        if (tid == 0) *okp = 0;
+        if (tid == 0) {
+            *okp = 0;
+            if (ack) __hip_atomic_store(&st->spare_ack, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return;
     }
     for (int t = tid; t < m * W; t += nt) {
@@ -3172,7 +3262,8 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
         A[t] = v;
     }
     if (tid == 0) ok_s = 1;
-    __syncthreads();
+    __syncthreads();   // every thread's loads have landed in LDS (and the state words in registers)
+    if (ack && tid == 0) __hip_atomic_store(&st->spare_ack, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int k = 0; k < m; ++k) {
         const double piv = A[k * W + k];
         if (!(piv > 0.0)) {
@@ -3209,8 +3300,11 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A) {
 // no LDS round trip -- round 4's first form read S, Iv and the vectors from LDS per product and took
 // ~3 us at m = 18, longer than the elimination.  On success r holds x.
 template <int MM>
-__device__ __forceinline__ bool small_refine_reg(const double* S, double* r, const double* Iv, int m, int lane) {
+__device__ __forceinline__ bool small_refine_reg(const double* S, double* r, const double* Iv, int m, int lane, int* corr) {
     const int li = lane < m ? lane : 0;
+    // a necessary condition for S > 0 that the direct elimination's pivots would test: a non-positive
+    // (or NaN) diagonal entry sends the system to gj_rows, which reports it (MCC_ENOTPD)
+    if (__builtin_amdgcn_ballot_w64(lane < m && !(S[li * m + li] > 0.0))) return false;
     double sr[MM], ir[MM];
 #pragma unroll
     for (int j = 0; j < MM; ++j) {
@@ -3240,6 +3334,7 @@ __device__ __forceinline__ bool small_refine_reg(const double* S, double* r, con
         conv = qm <= kTol;
         if (conv || it >= kWarmMaxIters || (it > 0 && !(qm <= 0.25 * qprev))) break;
         qprev = qm;
+        *corr = it + 1;
         double dx = 0.0;
 #pragma unroll
         for (int j = 0; j < MM; ++j)
@@ -3249,9 +3344,9 @@ __device__ __forceinline__ bool small_refine_reg(const double* S, double* r, con
     if (conv && lane < m) r[lane] = x;   // rr was read by every lane above (one wave: in order)
     return conv;
 }
-__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, int m, int lane) {
+__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, int m, int lane, int* corr) {
     switch (m) {
-#define SR(M) case M: return small_refine_reg<M>(S, r, Iv, m, lane);
+#define SR(M) case M: return small_refine_reg<M>(S, r, Iv, m, lane, corr);
         SR(6) SR(12) SR(18) SR(24) SR(30)
 #undef SR
         default: return false;
@@ -3271,6 +3366,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     __shared__ unsigned s_ep;
     SSTAMP(a.stamps, 0, 0);
     const bool wrm = LARGE && warm_on(warm, m);
+    __shared__ int s_sm_ok, s_sm_corr;   // m <= 30: the refinement converged, with this many corrections
     WarmStage ws;
     if (wrm) warm_issue(S, m, ws);
     if (wrm && tid == 64) warm_check(*warm, &s_use, &s_ep);
@@ -3308,7 +3404,13 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         if (tid == 64) s_bad_rows = 0;   // (this wave's own write below follows in program order)
         // with the previous system's inverse (k_schur, m <= 30): refinement, else / on failure the
         // register Gauss-Jordan
-        if (!(Iv && small_refine(S, r, Iv, m, tid - 64))) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
+        int corr = 0;
+        const bool ok = Iv && small_refine(S, r, Iv, m, tid - 64, &corr);
+        if (tid == 64) {   // (statistics, read after the barriers below)
+            s_sm_ok = ok;
+            s_sm_corr = corr;
+        }
+        if (!ok) gj_dispatch(S, r, m, tid - 64, &st->error, &s_bad_rows);
         SSTAMP(a.stamps, 2, 64);
     }
     __syncthreads();
@@ -3367,6 +3469,16 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         if (s_err0 & kErrPhotoNotPD) atomicOr(&st->error, kErrPhotoNotPD);   // another rank's photo
         st->done = 1;
         if (warm) warm_stop(*warm);
+    }
+    if (!LARGE && tid == 64 && a.sstats) {   // m <= 30 warm-solve statistics, last (nothing waits on them)
+        unsigned long long* ss = reinterpret_cast<unsigned long long*>(a.sstats);
+        if (Iv) {
+            atomicAdd(ss + 0, 1ull);
+            atomicAdd(ss + 1, (unsigned long long)s_sm_corr);
+            if (!s_sm_ok) atomicAdd(ss + 2, 1ull);
+        } else {
+            atomicAdd(ss + 3, 1ull);
+        }
     }
 }
 
@@ -3862,7 +3974,7 @@ __device__ __forceinline__ void rod_f32(const float* r, float* Rf) {
     for (int k = 0; k < 9; ++k) Rf[k] = (float)o.R[k];
 }
 
-template <int MODEL, bool RATIONAL, bool PRISM>
+template <int MODEL, bool RATIONAL, int PRISM>
 __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 #pragma clang fp contract(off)
     const int e = blockIdx.x;   // photo-major edge index
@@ -3956,7 +4068,8 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
         if (MODEL == MCC_MODEL_OMNI)
             omni_corner(R, T, kd, fx, fy, cx, cy, sk, (double)a.xi[cam], a.obj_x[c], a.obj_y[c], a.obj_z[c], Yr, u, v, D);
         else
-            pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, a.obj_x[c], a.obj_y[c], a.obj_z[c], Yr, u, v, D);
+            pinhole_corner<RATIONAL, PRISM>(R, T, kd, fx, fy, cx, cy, a.obj_x[c], a.obj_y[c], a.obj_z[c], Yr, u, v, D,
+                                            PRISM == 2 ? a.tilt + 9 * cam : nullptr);
         const float ex = a.img_u[c] - u, ey = a.img_v[c] - v;
         float s2 = ex * ex;
         s2 = s2 + ey * ey;
@@ -3979,8 +4092,9 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 using namespace mcc;
 
 template <int MODEL>
-static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, bool prism) {
+static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, int prism) {
     const dim3 grid(n_photos + (a.ssinv ? 1 : 0));   // + the m <= 30 warm solve's spare workgroup
+    if (prism == 2) return hipErrorInvalidValue;   // the tilted sensor takes the split step (mcc_create)
     if (rational && prism) hipLaunchKernelGGL((k_linearize<MODEL, true, true>), grid, dim3(256), shmem, s, a);
     else if (rational) hipLaunchKernelGGL((k_linearize<MODEL, true, false>), grid, dim3(256), shmem, s, a);
     else if (prism) hipLaunchKernelGGL((k_linearize<MODEL, false, true>), grid, dim3(256), shmem, s, a);
@@ -3994,12 +4108,12 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
 #define MCC_EDGE_LANES 16
 #endif
 constexpr int kEdgeLanes = MCC_EDGE_LANES;   // lanes per edge in k_edge (16 or 8)
-template <int MODEL, bool RATIONAL, bool PRISM>
+template <int MODEL, bool RATIONAL, int PRISM>
 static void launch_edge(const LinArgs& a, hipStream_t s) {
     constexpr int per = 64 / kEdgeLanes;
     hipLaunchKernelGGL((k_edge<MODEL, RATIONAL, PRISM, kEdgeLanes>), dim3((a.n_edges + per - 1) / per), dim3(64), 0, s, a);
 }
-hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, bool prism, size_t photo_shmem,
+hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, int prism, size_t photo_shmem,
                             hipStream_t s) {
     if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
     const dim3 gp((a.n_photos + 64 / kPrepGroup - 1) / (64 / kPrepGroup));
@@ -4014,7 +4128,8 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, bool pri
     } else if (model == MCC_MODEL_DOUBLESIDE) {
         if (p4) hipLaunchKernelGGL((k_prep4<MCC_MODEL_DOUBLESIDE, true>), g4, dim3(64), p4shm, s, a);
         else hipLaunchKernelGGL((k_prep<MCC_MODEL_DOUBLESIDE, true>), gp, dim3(64), 0, s, a);
-        if (rational && prism) launch_edge<MCC_MODEL_DOUBLESIDE, true, true>(a, s);
+        if (prism == 2) launch_edge<MCC_MODEL_DOUBLESIDE, true, 2>(a, s);
+        else if (rational && prism) launch_edge<MCC_MODEL_DOUBLESIDE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_DOUBLESIDE, true, false>(a, s);
         else if (prism) launch_edge<MCC_MODEL_DOUBLESIDE, false, true>(a, s);
         else launch_edge<MCC_MODEL_DOUBLESIDE, false, false>(a, s);
@@ -4023,7 +4138,8 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, bool pri
         else if (p4) hipLaunchKernelGGL((k_prep4<MCC_MODEL_PINHOLE, false>), g4, dim3(64), p4shm, s, a);
         else if (a.has_back) hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, true>), gp, dim3(64), 0, s, a);
         else hipLaunchKernelGGL((k_prep<MCC_MODEL_PINHOLE, false>), gp, dim3(64), 0, s, a);
-        if (rational && prism) launch_edge<MCC_MODEL_PINHOLE, true, true>(a, s);
+        if (prism == 2) launch_edge<MCC_MODEL_PINHOLE, true, 2>(a, s);
+        else if (rational && prism) launch_edge<MCC_MODEL_PINHOLE, true, true>(a, s);
         else if (rational) launch_edge<MCC_MODEL_PINHOLE, true, false>(a, s);
         else if (prism) launch_edge<MCC_MODEL_PINHOLE, false, true>(a, s);
         else launch_edge<MCC_MODEL_PINHOLE, false, false>(a, s);
@@ -4048,7 +4164,7 @@ size_t mcc_solve_shmem(int m) {
     return std::max((size_t)(m * m + m), m > 30 ? std::max(blocked, warm) : 0) * sizeof(double);
 }
 
-hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, bool prism, hipStream_t s) {
+hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, int prism, hipStream_t s) {
     const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.max_cpp);
     switch (model) {
         case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
@@ -4057,7 +4173,7 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
     }
 }
 
-template <int MODEL, bool RATIONAL, bool PRISM, bool BACK, int L>
+template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
     // + the spare workgroup of the m <= 30 warm solve (small_inverse)
     hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), dim3(a.n_pgroups + (a.ssinv ? 1 : 0)),
@@ -4065,26 +4181,29 @@ static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) 
     return hipGetLastError();
 }
 template <int L>
-static hipError_t launch_group_l(const LinArgs& a, int model, bool rational, bool prism, size_t shmem, hipStream_t s) {
+static hipError_t launch_group_l(const LinArgs& a, int model, bool rational, int prism, size_t shmem, hipStream_t s) {
     if (model == MCC_MODEL_OMNI) return launch_group_t<MCC_MODEL_OMNI, false, false, false, L>(a, shmem, s);
     if (model == MCC_MODEL_DOUBLESIDE) {
+        if (prism == 2) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, 2, true, L>(a, shmem, s);
         if (rational && prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, true, true, L>(a, shmem, s);
         if (rational) return launch_group_t<MCC_MODEL_DOUBLESIDE, true, false, true, L>(a, shmem, s);
         if (prism) return launch_group_t<MCC_MODEL_DOUBLESIDE, false, true, true, L>(a, shmem, s);
         return launch_group_t<MCC_MODEL_DOUBLESIDE, false, false, true, L>(a, shmem, s);
     }
     if (a.has_back) {
+        if (prism == 2) return launch_group_t<MCC_MODEL_PINHOLE, true, 2, true, L>(a, shmem, s);
         if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, true, L>(a, shmem, s);
         if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, true, L>(a, shmem, s);
         if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, true, L>(a, shmem, s);
         return launch_group_t<MCC_MODEL_PINHOLE, false, false, true, L>(a, shmem, s);
     }
+    if (prism == 2) return launch_group_t<MCC_MODEL_PINHOLE, true, 2, false, L>(a, shmem, s);
     if (rational && prism) return launch_group_t<MCC_MODEL_PINHOLE, true, true, false, L>(a, shmem, s);
     if (rational) return launch_group_t<MCC_MODEL_PINHOLE, true, false, false, L>(a, shmem, s);
     if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, false, L>(a, shmem, s);
     return launch_group_t<MCC_MODEL_PINHOLE, false, false, false, L>(a, shmem, s);
 }
-hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, bool prism, int lanes, size_t shmem,
+hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, int prism, int lanes, size_t shmem,
                             hipStream_t s) {
     if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
     return lanes == 32 ? launch_group_l<32>(a, model, rational, prism, shmem, s)
@@ -4098,7 +4217,8 @@ static hipError_t set_group_attrs(size_t group_shmem) {
                          SETG(2, false, true, true), SETG(2, false, false, true), SETG(0, true, true, true),
                          SETG(0, true, false, true), SETG(0, false, true, true), SETG(0, false, false, true),
                          SETG(0, true, true, false), SETG(0, true, false, false), SETG(0, false, true, false),
-                         SETG(0, false, false, false)})
+                         SETG(0, false, false, false), SETG(2, true, 2, true), SETG(0, true, 2, true),
+                         SETG(0, true, 2, false)})
         if (e != hipSuccess) err = e;
 #undef SETG
     return err;
@@ -4203,13 +4323,13 @@ hipError_t mcc_launch_backsub(const BacksubArgs& a, hipStream_t s) {
     if (a.n_photos > 0) hipLaunchKernelGGL(k_backsub, dim3((a.n_photos + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t mcc_launch_project_error(const ErrArgs& a, int model, int n_edges, bool rational, bool prism, hipStream_t s) {
+hipError_t mcc_launch_project_error(const ErrArgs& a, int model, int n_edges, bool rational, int prism, hipStream_t s) {
 #define PE(M, R, P) hipLaunchKernelGGL((k_project_error<M, R, P>), dim3(n_edges), dim3(64), 0, s, a)
     if (model == MCC_MODEL_OMNI) PE(1, false, false);
     else if (model == MCC_MODEL_DOUBLESIDE) {
-        if (rational && prism) PE(2, true, true); else if (rational) PE(2, true, false); else if (prism) PE(2, false, true); else PE(2, false, false);
+        if (prism == 2) PE(2, true, 2); else if (rational && prism) PE(2, true, true); else if (rational) PE(2, true, false); else if (prism) PE(2, false, true); else PE(2, false, false);
     } else {
-        if (rational && prism) PE(0, true, true); else if (rational) PE(0, true, false); else if (prism) PE(0, false, true); else PE(0, false, false);
+        if (prism == 2) PE(0, true, 2); else if (rational && prism) PE(0, true, true); else if (rational) PE(0, true, false); else if (prism) PE(0, false, true); else PE(0, false, false);
     }
 #undef PE
     return hipGetLastError();

@@ -102,10 +102,31 @@ void log_of(const double* R, double r[3]) {
     r[0] = rx; r[1] = ry; r[2] = rz;
 }
 
+// computeTiltProjectionMatrix (OpenCV calib3d): matTilt = matProjZ * (matRotY(tau_y) * matRotX(tau_x))
+void tilt_of(double tx, double ty, double M[9]) {
+    const double cx = std::cos(tx), sx = std::sin(tx), cy = std::cos(ty), sy = std::sin(ty);
+    const double rx[9] = {1, 0, 0, 0, cx, sx, 0, -sx, cx}, ry[9] = {cy, 0, -sy, 0, 1, 0, sy, 0, cy};
+    double rxy[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int q = 0; q < 3; ++q) s += ry[3 * i + q] * rx[3 * q + j];
+            rxy[3 * i + j] = s;
+        }
+    const double pz[9] = {rxy[8], 0, -rxy[2], 0, rxy[8], -rxy[5], 0, 0, 1};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int q = 0; q < 3; ++q) s += pz[3 * i + q] * rxy[3 * q + j];
+            M[3 * i + j] = s;
+        }
+}
+
 // One corner through cv::projectPoints' pinhole model (cvProjectPoints2Internal, k1 k2 p1 p2 [k3
-// [k4 k5 k6 [s1 s2 s3 s4]]], no tilt): the float32 pixel and D = d(u, v)/dXc (2 x 3)
+// [k4 k5 k6 [s1 s2 s3 s4 [tau_x tau_y]]]]): the float32 pixel and D = d(u, v)/dXc (2 x 3).  mt: the
+// tilted sensor's matTilt (null: none) -- vecTilt = mt (xd0, yd0, 1), (xd, yd) = vecTilt(0..1) / vecTilt(2)
 void pinhole_point(const double* R, const double* T, const double* k, const float* Kf, const float* P, float& u,
-                   float& v, double* Yr, double* D) {
+                   float& v, double* Yr, double* D, const double* mt) {
     const double fx = Kf[0], fy = Kf[4], cx = Kf[2], cy = Kf[5];
     const double X = P[0], Y = P[1], Z = P[2];
     Yr[0] = R[0] * X + R[1] * Y + R[2] * Z;
@@ -119,8 +140,17 @@ void pinhole_point(const double* R, const double* T, const double* k, const floa
     const double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
     const double cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
     const double icdist2 = 1. / (1 + k[5] * r2 + k[6] * r4 + k[7] * r6);
-    const double xd = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
-    const double yd = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
+    double xd = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
+    double yd = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
+    double t0 = 0, t1 = 0, t2 = 1, ip = 1;
+    if (mt) {
+        t0 = mt[0] * xd + mt[1] * yd + mt[2];
+        t1 = mt[3] * xd + mt[4] * yd + mt[5];
+        t2 = mt[6] * xd + mt[7] * yd + mt[8];
+        ip = t2 ? 1. / t2 : 1;
+        xd = ip * t0;
+        yd = ip * t1;
+    }
     u = (float)(xd * fx + cx);
     v = (float)(yd * fy + cy);
     // the distortion map's derivative w.r.t. the normalised point, then d(x, y)/dXc
@@ -128,10 +158,18 @@ void pinhole_point(const double* R, const double* T, const double* k, const floa
     const double g = (k[0] + 2 * k[1] * r2 + 3 * k[4] * r4) * icdist2 -
                      cdist * icdist2 * icdist2 * (k[5] + 2 * k[6] * r2 + 3 * k[7] * r4);
     const double P1 = k[8] + 2 * r2 * k[9], P2 = k[10] + 2 * r2 * k[11];
-    const double m00 = cc + 2 * x * x * g + 2 * k[2] * y + 6 * k[3] * x + 2 * x * P1;
-    const double m01 = 2 * x * y * g + 2 * k[2] * x + 2 * k[3] * y + 2 * y * P1;
-    const double m10 = 2 * x * y * g + 2 * k[2] * x + 2 * k[3] * y + 2 * x * P2;
-    const double m11 = cc + 2 * y * y * g + 6 * k[2] * y + 2 * k[3] * x + 2 * y * P2;
+    double m00 = cc + 2 * x * x * g + 2 * k[2] * y + 6 * k[3] * x + 2 * x * P1;
+    double m01 = 2 * x * y * g + 2 * k[2] * x + 2 * k[3] * y + 2 * y * P1;
+    double m10 = 2 * x * y * g + 2 * k[2] * x + 2 * k[3] * y + 2 * x * P2;
+    double m11 = cc + 2 * y * y * g + 6 * k[2] * y + 2 * k[3] * x + 2 * y * P2;
+    if (mt) {   // dMatTilt (2 x 2) after the distortion map
+        const double ip2 = ip * ip;
+        const double d00 = (mt[0] * t2 - mt[6] * t0) * ip2, d01 = (mt[1] * t2 - mt[7] * t0) * ip2;
+        const double d10 = (mt[3] * t2 - mt[6] * t1) * ip2, d11 = (mt[4] * t2 - mt[7] * t1) * ip2;
+        const double n00 = d00 * m00 + d01 * m10, n01 = d00 * m01 + d01 * m11;
+        const double n10 = d10 * m00 + d11 * m10, n11 = d10 * m01 + d11 * m11;
+        m00 = n00; m01 = n01; m10 = n10; m11 = n11;
+    }
     const double fzx = fx * z, fzy = fy * z;
     D[0] = fzx * m00;
     D[1] = fzx * m01;
@@ -213,8 +251,6 @@ void edgeJacobian(int edgeClass, bool omni, int patternSide, const double rP[3],
     if (!omni && !(nd == 4 || nd == 5 || nd == 8 || nd == 12 || nd == 14))
         throw std::invalid_argument("edgeJacobian: pinhole distortion must have 4, 5, 8, 12 or 14 terms");
     if (omni && nd != 4) throw std::invalid_argument("edgeJacobian: omnidir distortion must have 4 terms");
-    if (!omni && nd == 14 && (D[12] != 0.f || D[13] != 0.f))
-        throw std::invalid_argument("edgeJacobian: tilted-sensor distortion (tau_x, tau_y != 0) is not supported");
     const bool back = patternSide == MultiCameraCalibration::BACK_PATTERN && edgeClass != EDGE_BASE;
     if (back && (!rDs || !tDs)) throw std::invalid_argument("edgeJacobian: a BACK view needs the double-side transform");
 
@@ -272,6 +308,9 @@ void edgeJacobian(int edgeClass, bool omni, int patternSide, const double rP[3],
     so3_jac(rf, +1.0, false, Jl);
     double kd[12] = {0};
     for (int q = 0; q < nd && q < 12; ++q) kd[q] = D[q];
+    double mt[9];   // the tilted sensor (14 terms, tau != 0)
+    const bool tilt = !omni && nd == 14 && (D[12] != 0.f || D[13] != 0.f);
+    if (tilt) tilt_of(D[12], D[13], mt);
 
     out.jacPhoto.assign(12 * (size_t)n, 0.0);
     out.jacGlobal.assign(12 * (size_t)n, 0.0);
@@ -281,7 +320,7 @@ void edgeJacobian(int edgeClass, bool omni, int patternSide, const double rP[3],
         float u, v;
         double Yr[3], Dp[6];
         if (omni) omni_point(R, tf, kd, K, (double)xi, obj + 3 * (size_t)i, u, v, Yr, Dp);
-        else pinhole_point(R, tf, kd, K, obj + 3 * (size_t)i, u, v, Yr, Dp);
+        else pinhole_point(R, tf, kd, K, obj + 3 * (size_t)i, u, v, Yr, Dp, tilt ? mt : nullptr);
         out.proj[2 * (size_t)i] = u;
         out.proj[2 * (size_t)i + 1] = v;
         const float eu = img[2 * (size_t)i] - u, ev = img[2 * (size_t)i + 1] - v;   // fl32(obs - proj)

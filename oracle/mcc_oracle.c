@@ -267,13 +267,43 @@ void ora_compose_motion(const double om1[3], const double T1[3], const double om
 
 /* ------------------------------------------------------------------ projection models */
 
+/* computeTiltProjectionMatrix (OpenCV calib3d distortion_model.hpp): matTilt = matProjZ * matRotXY,
+ * matRotXY = matRotY(tauY) * matRotX(tauX), matProjZ = [[r22, 0, -r02], [0, r22, -r12], [0, 0, 1]]
+ * (r = matRotXY); cv::Matx products sum from 0, left to right. */
+void ora_tilt_matrix(double tauX, double tauY, double M[9])
+{
+    double cTauX = cos(tauX), sTauX = sin(tauX), cTauY = cos(tauY), sTauY = sin(tauY);
+    double rx[9] = {1, 0, 0, 0, cTauX, sTauX, 0, -sTauX, cTauX};
+    double ry[9] = {cTauY, 0, -sTauY, 0, 1, 0, sTauY, 0, cTauY};
+    double rxy[9], pz[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int q = 0; q < 3; ++q) s += ry[3 * i + q] * rx[3 * q + j];
+            rxy[3 * i + j] = s;
+        }
+    pz[0] = rxy[8]; pz[1] = 0; pz[2] = -rxy[2];
+    pz[3] = 0; pz[4] = rxy[8]; pz[5] = -rxy[5];
+    pz[6] = 0; pz[7] = 0; pz[8] = 1;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double s = 0;
+            for (int q = 0; q < 3; ++q) s += pz[3 * i + q] * rxy[3 * q + j];
+            M[3 * i + j] = s;
+        }
+}
+
 int ora_project_pinhole(int n, const float *obj, const float rvec[3], const float tvec[3],
                         const float Kf[9], const float *Df, int nd, float *img, double *jac)
 {
-    /* cv::projectPoints -> cvProjectPoints2Internal (OpenCV 4.x), aspectRatio = 0. */
+    /* cv::projectPoints -> cvProjectPoints2Internal (OpenCV 4.x), aspectRatio = 0.  With 14
+     * coefficients the tilted-sensor projection follows the distortion: vecTilt = matTilt *
+     * (xd0, yd0, 1), invProj = 1 / vecTilt(2), (xd, yd) = invProj * vecTilt(0..1); the derivatives
+     * pass through dMatTilt(r, c) = (matTilt(r, c) vecTilt(2) - matTilt(2, c) vecTilt(r)) invProj^2. */
     double k[14] = {0};
     for (int i = 0; i < nd && i < 14; ++i) k[i] = Df[i];
-    if (k[12] != 0 || k[13] != 0) return -1; /* tilted sensor model not restated */
+    double mt[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    if (nd == 14) ora_tilt_matrix(k[12], k[13], mt);
     double r[3] = {rvec[0], rvec[1], rvec[2]}, t[3] = {tvec[0], tvec[1], tvec[2]};
     double R[9], dRdr[27];
     ora_rodrigues_v2m(r, R, dRdr);
@@ -289,9 +319,20 @@ int ora_project_pinhole(int n, const float *obj, const float rvec[3], const floa
         double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
         double cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
         double icdist2 = 1. / (1 + k[5] * r2 + k[6] * r4 + k[7] * r6);
-        double xd = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
-        double yd = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
-        /* tilt = identity (tau = 0): vecTilt = (xd, yd, 1), invProj = 1 */
+        double xd0 = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
+        double yd0 = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
+        double vt0 = 0, vt1 = 0, vt2 = 0;
+        vt0 += mt[0] * xd0; vt0 += mt[1] * yd0; vt0 += mt[2] * 1.0;
+        vt1 += mt[3] * xd0; vt1 += mt[4] * yd0; vt1 += mt[5] * 1.0;
+        vt2 += mt[6] * xd0; vt2 += mt[7] * yd0; vt2 += mt[8] * 1.0;
+        double invProj = vt2 ? 1. / vt2 : 1;
+        double xd = invProj * vt0, yd = invProj * vt1;
+        double dmt[4];   /* dMatTilt (2 x 2, row-major) */
+        for (int row = 0; row < 2; ++row)
+            for (int col = 0; col < 2; ++col)
+                dmt[2 * row + col] = mt[3 * row + col] * vt2 - mt[6 + col] * (row ? vt1 : vt0);
+        double ips = invProj * invProj;
+        for (int q = 0; q < 4; ++q) dmt[q] *= ips;
         img[2 * i] = (float)(xd * fx + cx);
         img[2 * i + 1] = (float)(yd * fy + cy);
         if (jac) {
@@ -313,8 +354,8 @@ int ora_project_pinhole(int n, const float *obj, const float rvec[3], const floa
                                 k[2] * da1dr + k[3] * (dr2dr + 4 * x * dxdr) + (k[8] + 2 * r2 * k[9]) * dr2dr);
                 double dmydr = (dydr * cdist * icdist2 + y * dcdist_dr * icdist2 + y * cdist * dicdist2_dr +
                                 k[2] * (dr2dr + 4 * y * dydr) + k[3] * da1dr + (k[10] + 2 * r2 * k[11]) * dr2dr);
-                ju[j] = fx * dmxdr;
-                jv[j] = fy * dmydr;
+                ju[j] = fx * (dmt[0] * dmxdr + dmt[1] * dmydr);
+                jv[j] = fy * (dmt[2] * dmxdr + dmt[3] * dmydr);
             }
             double dxdt[3] = {z, 0, -x * z}, dydt[3] = {0, z, -y * z};
             for (int j = 0; j < 3; ++j) {
@@ -326,8 +367,8 @@ int ora_project_pinhole(int n, const float *obj, const float rvec[3], const floa
                                 k[2] * da1dt + k[3] * (dr2dt + 4 * x * dxdt[j]) + (k[8] + 2 * r2 * k[9]) * dr2dt);
                 double dmydt = (dydt[j] * cdist * icdist2 + y * dcdist_dt * icdist2 + y * cdist * dicdist2_dt +
                                 k[2] * (dr2dt + 4 * y * dydt[j]) + k[3] * da1dt + (k[10] + 2 * r2 * k[11]) * dr2dt);
-                ju[3 + j] = fx * dmxdt;
-                jv[3 + j] = fy * dmydt;
+                ju[3 + j] = fx * (dmt[0] * dmxdt + dmt[1] * dmydt);
+                jv[3 + j] = fy * (dmt[2] * dmxdt + dmt[3] * dmydt);
             }
         }
     }

@@ -74,7 +74,11 @@ void ora_rodrigues_m2v(const double R[9], double r[3], double J[27]);
 void ora_compose_motion(const double om1[3], const double T1[3], const double om2[3],
                         const double T2[3], double om3[3], double T3[3], double d[8][9]);
 
-/* cv::projectPoints (pinhole, CV_32F object points -> CV_32F image points).
+/* computeTiltProjectionMatrix: the tilted sensor's matTilt (3 x 3 row-major) for tau_x, tau_y */
+void ora_tilt_matrix(double tauX, double tauY, double M[9]);
+
+/* cv::projectPoints (pinhole, CV_32F object points -> CV_32F image points; nd 4, 5, 8, 12 or 14, the
+ * last with the tilted-sensor projection).
  * jac (optional): 2n x 6 row-major, columns [d/drvec(3), d/dtvec(3)], rows u0,v0,u1,v1,... */
 int ora_project_pinhole(int n, const float *obj, const float rvec[3], const float tvec[3],
                         const float K[9], const float *D, int nd, float *img, double *jac);

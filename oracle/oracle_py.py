@@ -190,6 +190,13 @@ def project_pinhole(obj, rvec, tvec, K, D, jac=True):
     return img.reshape(n, 2), J
 
 
+def tilt_matrix(tau_x, tau_y):
+    """computeTiltProjectionMatrix (ora_tilt_matrix): the tilted sensor's matTilt, 3 x 3."""
+    M = np.zeros(9)
+    lib().ora_tilt_matrix(ctypes.c_double(float(tau_x)), ctypes.c_double(float(tau_y)), _p(M, _f64p))
+    return M.reshape(3, 3)
+
+
 def project_omni(obj, rvec, tvec, K, xi, D, jac=True):
     obj = np.ascontiguousarray(obj, np.float32)
     n = obj.shape[0]

@@ -68,7 +68,7 @@ def project_pinhole(X, om, T, K, D):
     K = np.asarray(K, np.float64).reshape(3, 3)
     k = np.zeros(12)
     D = np.asarray(D, np.float64).ravel()
-    k[:D.size] = D
+    k[:min(D.size, 12)] = D[:12]
     k1, k2, p1, p2, k3, k4, k5, k6, s1, s2, s3, s4 = k
     Xc = X @ rodrigues(om).T + np.asarray(T, np.float64)
     z = np.where(Xc[:, 2] != 0, 1.0 / Xc[:, 2], 1.0)
@@ -80,6 +80,17 @@ def project_pinhole(X, om, T, K, D):
     a1, a2, a3 = 2 * x * y, r2 + 2 * x * x, r2 + 2 * y * y
     xd = x * cdist * icd + p1 * a1 + p2 * a2 + s1 * r2 + s2 * r4
     yd = y * cdist * icd + p1 * a3 + p2 * a1 + s3 * r2 + s4 * r4
+    if D.size == 14 and (D[12] != 0 or D[13] != 0):
+        # the tilted image sensor, from the model's definition (OpenCV camera model docs): the
+        # distorted point on the plane z = 1, rotated by R(tau) = Ry(tau_y) Rx(tau_x), then projected
+        # along the rotated optical axis back onto that plane: [[R33, 0, -R13], [0, R33, -R23], [0, 0, 1]]
+        tx, ty = D[12], D[13]
+        Rx = np.array([[1, 0, 0], [0, np.cos(tx), np.sin(tx)], [0, -np.sin(tx), np.cos(tx)]])
+        Ry = np.array([[np.cos(ty), 0, -np.sin(ty)], [0, 1, 0], [np.sin(ty), 0, np.cos(ty)]])
+        Rt = Ry @ Rx
+        w = np.stack([xd, yd, np.ones_like(xd)], 1) @ Rt.T
+        xd = Rt[2, 2] * w[:, 0] / w[:, 2] - Rt[0, 2]
+        yd = Rt[2, 2] * w[:, 1] / w[:, 2] - Rt[1, 2]
     return np.stack([K[0, 0] * xd + K[0, 2], K[1, 1] * yd + K[1, 2]], 1)
 
 

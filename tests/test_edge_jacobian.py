@@ -75,7 +75,34 @@ def _edge_inputs(p, x, e):
 def test_edge_jacobian_matches_oracle(host, path):
     gd = dict(np.load(path))
     p = rig.problem_from_arrays(gd)
-    x = np.asarray(gd["x0"], np.float32)
+    _check_problem(host, p, np.asarray(gd["x0"], np.float32), path)
+
+
+def _tilted(p):
+    """the 14-term model with the tilted sensor (tau_x, tau_y != 0, per camera)"""
+    D = np.zeros((p.n_cams, 14), np.float32)
+    D[:, :p.nd] = p.D
+    D[:, 5:12] = [0.01, -0.005, 0.002, 3e-4, -2e-4, 1e-4, 2e-4]
+    D[:, 12] = 0.01 * (1 + 0.1 * np.arange(p.n_cams))
+    D[:, 13] = -0.008 * (1 - 0.1 * np.arange(p.n_cams))
+    p.D = D
+    return p
+
+
+@pytest.mark.parametrize("name", ["front", "back"])
+def test_edge_jacobian_tilted_sensor(host, name):
+    """The tilted-sensor projection (nd = 14, tau != 0; cv::projectPoints at src/mymulticalib.cpp:566
+    with the camera XML's Distortion, :118-132) through the per-edge Jacobian, MyMulti front and BACK
+    views, against the oracle at the fixtures' bars."""
+    if name == "front":
+        p = rig.make_config("config2", n_views=12)
+    else:
+        p = rig.make_config("config5", n_views=8, model=rig.PINHOLE, double_sided=True)
+    p = _tilted(p)
+    _check_problem(host, p, p.x0, name)
+
+
+def _check_problem(host, p, x, path):
     o = O.Oracle(p)
     K = np.asarray(p.K, np.float32).reshape(-1, 9)
     D = np.asarray(p.D, np.float32).reshape(p.n_cams, -1)

@@ -38,6 +38,19 @@ def _widen_distortion(p, nd):
     return p
 
 
+def _tilt(p, tau=(0.01, -0.008)):
+    """the 14-term model with the tilted sensor (tau_x, tau_y != 0): cv::projectPoints at
+    src/mymulticalib.cpp:566 takes whatever Distortion the camera XML holds (:118-132); per camera a
+    slightly different tilt"""
+    p = _widen_distortion(p, 12)
+    D = np.zeros((p.n_cams, 14), np.float32)
+    D[:, :12] = p.D
+    D[:, 12] = tau[0] * (1 + 0.1 * np.arange(p.n_cams))
+    D[:, 13] = tau[1] * (1 - 0.1 * np.arange(p.n_cams))
+    p.D = D
+    return p
+
+
 def _omni_skew():
     p = rig.make_config("config4", n_views=30)
     K = p.K.copy()
@@ -60,16 +73,21 @@ CASES = {
     "nd8_rational": lambda: _widen_distortion(rig.make_config("config2", n_views=30), 8),
     "nd12_prism": lambda: _widen_distortion(rig.make_config("config2", n_views=30), 12),
     "omni_skew": _omni_skew,
+    "nd14_tilt": lambda: _tilt(rig.make_config("config2", n_views=30)),
+    "config5_tilt": lambda: _tilt(rig.make_config("config5", n_views=30)),
+    "pinhole_back_tilt": lambda: _tilt(rig.make_config("config5", n_views=30, model=rig.PINHOLE, double_sided=True)),
     "cams22_m126": lambda: rig.make_config("config3", n_cams=22, n_views=120),   # largest global block, 19 edges/photo
 }
 # the split step runs every m > 30 problem; these force it (MCC_FUSED=0) on the small-m models and
 # distortion variants the fused step otherwise takes.  "_split" takes the split step's default
 # linearisation kernel for the rig (k_group on these small rigs: groups fit the CUs), "_split3"
 # its three-kernel form (k_prep -> k_edge -> k_photo, MCC_GROUP=0; the larger rigs' default)
-SPLIT = ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd8_rational", "nd12_prism"]
+SPLIT = ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd8_rational", "nd12_prism",
+         "nd14_tilt", "config5_tilt", "pinhole_back_tilt"]
 for _n in SPLIT:
     CASES[_n + "_split"] = CASES[_n]
-for _n in ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd12_prism"]:
+for _n in ["config2_small", "config4_small", "config5_small", "pinhole_back", "nd12_prism", "nd14_tilt",
+           "config5_tilt", "pinhole_back_tilt"]:
     CASES[_n + "_split3"] = CASES[_n]
 CASES["config3_small_split3"] = CASES["config3_small"]
 # k_group at both lane widths: "_g16" its 256-thread form (16 lanes per edge), "_g32" the default

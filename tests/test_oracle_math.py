@@ -170,15 +170,20 @@ def test_project_pinhole_values_and_jacobian():
             assert np.abs(J - fd).max() < 1e-6 * np.abs(fd).max()
 
 
-@pytest.mark.parametrize("nd", [8, 12])
+@pytest.mark.parametrize("nd", [8, 12, 14])
 def test_project_pinhole_rational_prism(nd):
+    # nd = 14: the tilted sensor (tau_x, tau_y; cv::projectPoints reaches it at
+    # src/mymulticalib.cpp:566 with whatever Distortion the camera XML holds, :118-132), against the
+    # numpy model's geometric form of the tilt (rotate, re-project along the tilted axis)
     rng = np.random.default_rng(6 + nd)
     K = np.array([[1100, 0, 950], [0, 1120, 530], [0, 0, 1]], np.float32)
     D = np.zeros(nd, np.float32)
     D[:5] = [-0.1, 0.05, 3e-4, -2e-4, 0.01]
     D[5:8] = [0.02, -0.01, 0.005]
-    if nd == 12:
-        D[8:] = [1e-3, -5e-4, 8e-4, 2e-4]
+    if nd >= 12:
+        D[8:12] = [1e-3, -5e-4, 8e-4, 2e-4]
+    if nd == 14:
+        D[12:] = [0.02, -0.015]
     om = np.array([0.1, -0.2, 0.05], np.float32)
     T = np.array([30, -20, 1500], np.float32)
     X = (rng.uniform(-300, 300, size=(40, 3)) * [1, 1, 0]).astype(np.float32)
@@ -276,3 +281,29 @@ def test_edge_jacobians_fd(name):
         o_, n = int(p.edge_off[e]), int(p.edge_n[e])
         obs = p.img.reshape(-1)[2 * o_:2 * o_ + 2 * n]
         assert np.array_equal(E, (obs - proj).astype(np.float32).astype(np.float64))
+
+
+def test_tilt_zero_is_the_twelve_term_model():
+    """nd = 14 with tau = 0: matTilt is the identity and the projection (pixels and Jacobian) is
+    bitwise the 12-term one -- the identity tilt is exact in OpenCV's formula."""
+    rng = np.random.default_rng(21)
+    K = np.array([[1100, 0, 950], [0, 1120, 530], [0, 0, 1]], np.float32)
+    D12 = np.array([-0.1, 0.05, 3e-4, -2e-4, 0.01, 0.02, -0.01, 0.005, 1e-3, -5e-4, 8e-4, 2e-4], np.float32)
+    D14 = np.concatenate([D12, np.zeros(2, np.float32)])
+    om = np.array([0.1, -0.2, 0.05], np.float32)
+    T = np.array([30, -20, 1500], np.float32)
+    X = (rng.uniform(-300, 300, size=(40, 3)) * [1, 1, 0]).astype(np.float32)
+    a, Ja = O.project_pinhole(X, om, T, K, D12)
+    b, Jb = O.project_pinhole(X, om, T, K, D14)
+    assert np.array_equal(a, b) and np.array_equal(Ja, Jb)
+    M = O.tilt_matrix(0.0, 0.0)
+    assert np.array_equal(M, np.eye(3))
+    # matTilt for tau != 0: a homography that fixes the principal ray's image (the plane's origin)
+    # up to the tilt's shift, and is rotation-times-projection: det = R33^2 (numpy model's form)
+    tx, ty = 0.02, -0.015
+    M = O.tilt_matrix(tx, ty)
+    Rx = np.array([[1, 0, 0], [0, np.cos(tx), np.sin(tx)], [0, -np.sin(tx), np.cos(tx)]])
+    Ry = np.array([[np.cos(ty), 0, -np.sin(ty)], [0, 1, 0], [np.sin(ty), 0, np.cos(ty)]])
+    R = Ry @ Rx
+    P = np.array([[R[2, 2], 0, -R[0, 2]], [0, R[2, 2], -R[1, 2]], [0, 0, 1]])
+    assert np.allclose(M, P @ R, rtol=0, atol=1e-15)

@@ -135,20 +135,23 @@ def test_peer_ranks_one_device(case, world, tmp_path):
 
 
 @pytest.mark.gpu
-def test_warm_helper_delayed_on_one_rank(tmp_path):
-    """The m > 30 warm solve at world 2 with rank 1's helper holding every
-    inverse back by 3 ms (MCC_WARM_DELAY_US; the round-3 k_solve gave up after 0.5 ms and switched
-    that rank to the direct elimination).  Every rank solves the same bits by the same algorithm:
-    the global block is bit-identical on both ranks and bit-identical to the undelayed run, and the
-    oracle bars of test_peer_ranks_one_device hold (src/multicalib.cpp:462-514, the solve it
+@pytest.mark.parametrize("case,delay", [("config3_small", {"MCC_WARM_DELAY_US": "3000"}),
+                                        ("config2_small", {"MCC_SPARE_DELAY_US": "300"})])
+def test_warm_helper_delayed_on_one_rank(case, delay, tmp_path):
+    """The warm solves at world 2 with rank 1's inverse producer held back:
+    m > 30 (config3_small), the helper kernel holds every inverse back by 3 ms (MCC_WARM_DELAY_US; the
+    round-3 k_solve gave up after 0.5 ms and switched that rank to the direct elimination); m <= 30 on
+    the fused step (config2_small), the spare workgroup starts 300 us late (MCC_SPARE_DELAY_US), long
+    after its launch's final arriver reached the exchange.  Every rank solves the same bits by the same
+    algorithm: the global block is bit-identical on both ranks and bit-identical to the undelayed run,
+    and the oracle bars of test_peer_ranks_one_device hold (src/multicalib.cpp:462-514, the solve it
     replaces :565-592)."""
-    case = "config3_small"
     p = peer_worker.CASES[case]()
     m = p.global_dim
     (tmp_path / "base").mkdir()
     (tmp_path / "slow").mkdir()
     base = _run_ranks(case, 2, tmp_path / "base", steps=20)
-    slow = _run_ranks(case, 2, tmp_path / "slow", steps=20, rank_env={1: {"MCC_WARM_DELAY_US": "3000"}})
+    slow = _run_ranks(case, 2, tmp_path / "slow", steps=20, rank_env={1: delay})
     x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
     for r in slow:
         assert int(r["it"]) == it_ref

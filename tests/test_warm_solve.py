@@ -192,3 +192,88 @@ def test_small_m_warm_matches_direct_and_oracle(cfg, views, env):
         assert abs(m - m_ref) <= 1e-6
         assert f32_ulp_diff(x, x_ref).max() <= 1
     assert f32_ulp_diff(xw, xd).max() <= 1
+
+
+def _fused_runs(p, env):
+    """optimize (COUNT + EPS) and 24 free-running steps from x0 on a fresh problem; the solve stats"""
+    ba = make(p, env)
+    try:
+        assert ba.path() == "fused", ba.path()
+        x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+        s_opt = ba.solve_stats()
+        ba.set_params(p.x0)
+        ba.step(24)
+        ba.check()
+        xs = ba.get_params()
+        s_all = ba.solve_stats()
+    finally:
+        ba.close()
+    return x, it, xs, s_opt, s_all
+
+
+@pytest.mark.parametrize("views", [120, 512])
+def test_fused_spare_delayed_is_bitwise_the_undelayed_run(views):
+    """The fused step's m <= 30 warm solve does not depend on when its spare workgroup runs: the spare
+    acknowledges once it holds the previous launch's system, and the final arriver writes neither the
+    packed system nor the state before that (small_inverse / spare_wait).  A spare held back by
+    MCC_SPARE_DELAY_US = 300 us (ten steps' time: it starts long after the final arriver reached the
+    solve) gives bitwise the undelayed optimize and free-running steps, with the same refinement
+    statistics; only 'waited' differs.  512 views is the fused path's largest rig (V = 2 x CUs): a grid
+    of 513 workgroups, one more than the co-resident slots, so the spare starts only after a photo
+    exits.  Both runs repeat bitwise (a second undelayed run), and refine: every update step after
+    the first two has an inverse of the right iteration.  The loop is src/multicalib.cpp:462-514."""
+    p = rig.make_config("config2", n_views=views)
+    runs = [_fused_runs(p, env) for env in ({}, {}, {"MCC_SPARE_DELAY_US": "300"})]
+    (x0, it0, xs0, so0, sa0) = runs[0]
+    for (x, it, xs, so, sa) in runs[1:]:
+        assert it == it0
+        assert np.array_equal(x, x0) and np.array_equal(xs, xs0)
+        for k in ("warm", "corrections", "fallbacks", "direct"):
+            assert so[k] == so0[k] and sa[k] == sa0[k], (so0, so, sa0, sa)
+    assert so0["warm"] >= it0 - 3 and so0["warm"] > 0, (it0, so0)
+    assert runs[2][4]["waited"] > 0, runs[2][4]
+    assert runs[0][4]["waited"] == 0 or views == 512, runs[0][4]
+    x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    assert it0 == it_ref
+    assert f32_ulp_diff(x0, x_ref).max() <= (1 if views <= 120 else 2)
+
+
+def test_fused_spare_timeout_fails_the_step():
+    """A spare slower than the bound (MCC_SPARE_DELAY_US = 30 ms, MCC_WARM_TIMEOUT_MS = 3): the step
+    fails with MCC_ETIMEOUT (-6) before writing the system or the state, and a fresh problem recovers."""
+    p = rig.make_config("config2", n_views=60)
+    ba = make(p, {"MCC_SPARE_DELAY_US": "30000", "MCC_WARM_TIMEOUT_MS": "3"})
+    try:
+        with pytest.raises(api.MccError, match=r"\(-6\)"):
+            ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    finally:
+        ba.close()
+    x, m, it, _ = run(p, {})
+    x_ref, m_ref, it_ref, _ = O.Oracle(p).optimize(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    assert it == it_ref and abs(m - m_ref) <= 1e-6
+
+
+@pytest.mark.parametrize("cfg,views,env", [
+    ("config4", 200, {"MCC_FUSED": "0"}),                    # k_group -> k_schur (m = 18, spare)
+    ("config3", 48, {}),                                      # k_prep -> k_edge -> k_photo (m = 90, helper)
+])
+def test_timing_probe_keeps_the_trajectory(cfg, views, env):
+    """mcc_timing_linearize between free-running steps (bench.py's kernel timing): each probe launch
+    re-applies the pending photo update and rewrites Y' and z'; the probe restores them with the
+    parameters, so 10 steps + probe + 10 steps is bitwise 20 steps."""
+    p = rig.make_config(cfg, n_views=views)
+    out = []
+    for probe in (False, True):
+        ba = make(p, env)
+        try:
+            assert ba.path() == "split"
+            ba.set_params(p.x0)
+            ba.step(10)
+            if probe:
+                assert ba.timing_linearize(16) > 0
+            ba.step(10)
+            ba.check()
+            out.append(ba.get_params())
+        finally:
+            ba.close()
+    assert np.array_equal(out[0], out[1])
