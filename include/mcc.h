@@ -174,7 +174,9 @@ int mcc_peer_enable(mcc_problem *p, int on);
  * peer transport): a spare workgroup of the step's linearisation launch inverts the previous system,
  * and the final solve refines with it (the fused step: with the previous launch's, two updates stale);
  * the last field counts fused steps whose final arriver waited for the spare to acknowledge its inputs,
- * with the same MCC_WARM_TIMEOUT_MS bound.  All zero when the problem takes the direct elimination only
+ * with the same MCC_WARM_TIMEOUT_MS bound; the m <= 30 counters run only with MCC_SOLVE_STATS=1 at
+ * mcc_create (their atomics cost ~0.5 us per fused step).  All zero when the problem takes the direct
+ * elimination only
  * (m > 96, MCC_WARM=0, MCC_SMALL_WARM=0, RCCL on the fused step).  Which solve a step takes depends on
  * the systems only, never on timing. */
 int mcc_solve_stats(mcc_problem *p, long long *out);

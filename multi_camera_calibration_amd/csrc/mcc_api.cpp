@@ -227,6 +227,7 @@ struct mcc_problem {
     // k_solve may sit in a peer exchange before it publishes), the test delay (MCC_WARM_DELAY_US)
     long long warm_wait_ticks = 1000000000LL, warm_idle_ticks = 4000000000LL, warm_delay_ticks = 0;
     long long spare_delay_ticks = 0;  // MCC_SPARE_DELAY_US (test): the fused step's spare starts this late
+    bool small_stats = false;         // MCC_SOLVE_STATS=1: count the m <= 30 warm solves (SolveCtx::sstats)
     int fault_photo = -1;            // MCC_FAULT_PHOTO (test): LinArgs::fault_photo
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
@@ -290,7 +291,7 @@ namespace {
 
 mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
     mcc::SolveCtx c{p->state.p, p->alpha.p, (int)p->alpha.n, p->x.p, p->dg.p, p->delta.p, p->m, do_update};
-    c.sstats = p->ssinv.p ? p->warm_stats.p : nullptr;   // the m <= 30 warm solve's statistics
+    c.sstats = p->ssinv.p && p->small_stats ? p->warm_stats.p : nullptr;   // the m <= 30 warm solve's statistics
     return c;
 }
 
@@ -368,8 +369,12 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
     la.photo_norm = p->photo_norm.p;
     la.stamps = p->stamps.p;
     la.fault_photo = p->fault_photo;
-    la.ssinv = swarm ? p->ssinv.p : nullptr;
-    la.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
+    // (the fused step: update launches only -- the spare's acknowledgement is the launch's iteration + 1,
+    // distinct for the update launches of one optimisation, and a linearisation-only launch keeps the
+    // iteration; it solves by the direct elimination)
+    const bool lwarm = swarm && (do_update || !p->fused);
+    la.ssinv = lwarm ? p->ssinv.p : nullptr;
+    la.ssinv_ok = lwarm ? p->ssinv_ok.p : nullptr;
     la.spare_wait = p->warm_wait_ticks;
     la.spare_delay = p->spare_delay_ticks;
     // any RCCL communicator (also 1 rank: the GPU tests exercise this path on one device) takes the
@@ -561,7 +566,7 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     p->h_state->eps = eps;
     p->h_state->error = 0;
     // the fused step's spare protocol restarts (the stream is idle: no spare of an earlier launch runs)
-    p->h_state->spare_seq = p->h_state->spare_ack = 0;
+    p->h_state->spare_ack = 0;
     HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     return MCC_OK;
 }
@@ -1037,6 +1042,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
     if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
     if (const char* f = std::getenv("MCC_SPARE_DELAY_US")) p->spare_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
+    if (const char* f = std::getenv("MCC_SOLVE_STATS")) p->small_stats = std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_FAULT_PHOTO")) p->fault_photo = std::atoi(f);
     {
         double peer_ms = 30000.0;   // the helper outlives a k_solve's longest wait at a peer exchange

@@ -24,11 +24,12 @@ struct State {
     int pending;      // a solved photo update waits to be applied by the next k_linearize
     unsigned int epoch;   // peer exchanges completed (monotonic over the problem's life)
     long long xchg_ticks; // s_memrealtime ticks (100 MHz) inside peer exchanges, summed (monotonic)
-    // the fused step's m <= 30 warm solve (k_linearize's spare workgroup, small_inverse): fused launches
-    // since set_state (the final arriver advances it), and the spare's acknowledgement -- spare_seq + 1
-    // once it holds this launch's inputs (state words, the packed system) in LDS.  The final arriver
-    // writes neither the packed system nor the state before it has seen that acknowledgement.
-    unsigned int spare_seq, spare_ack;
+    // the fused step's m <= 30 warm solve (k_linearize's spare workgroup, small_inverse): the spare's
+    // acknowledgement of an update launch -- iter + 1 once it holds the launch's inputs (state words,
+    // the packed system) in LDS; the launch's final arriver writes neither the packed system nor the
+    // state before it has seen it.  Update launches of one optimisation have distinct iter, and
+    // set_state clears the word (no launch in flight), so an acknowledgement is never a stale one.
+    unsigned int spare_ack;
 };
 // State::error bits
 constexpr int kErrPhotoNotPD = 1;    // a photo's 6 x 6 block (any rank: summed through the exchange)
@@ -59,9 +60,10 @@ struct SolveCtx {
     double* delta;    // [P]
     int m, do_update;
     long long* stamps;   // MCC_DIAG: solve phase stamps (set by k_schur's last arriver)
-    // m <= 30 warm solve statistics (mcc_solve_stats, the m > 30 helper's layout): refinements tried,
+    // m <= 30 warm-solve statistics (mcc_solve_stats, the m > 30 helper's layout): refinements tried,
     // corrections, refinements that fell back to the elimination, eliminations without an inverse,
-    // fused steps whose final arriver waited for the spare's acknowledgement (null: off)
+    // fused steps whose final arriver waited for the spare.  Null unless MCC_SOLVE_STATS=1: the
+    // counters' atomics at the end of the solving workgroup cost ~0.5 us per config2 step
     long long* sstats;
 };
 

@@ -236,9 +236,7 @@ struct PhotoLds {
     double dgl[128];     // global-block delta of the previous solve (pending update)
     double nrm[2];       // ||G||^2, ||x||^2 of this photo's last applied update (fused step)
     double cn[2];        // state snapshot: camera-block ||G||^2, ||x||^2 of the last update
-    int iter0;           // state snapshot: completed updates
-    unsigned seq0;       // state snapshot: State::spare_seq (the fused step's spare acknowledgement)
-    int pad1[2];
+    int iter0, pad1[3];  // state snapshot: completed updates
     int bn[8];           // per camera block: number of the photo's edges in it (fused step)
     unsigned char bl[5][64];   // per camera block: those edges in edge order
     // followed by the camera table [C][kCamStride], the intrinsics [C][kIntrStride] and the
@@ -942,13 +940,14 @@ __device__ __forceinline__ unsigned ld_agent_u32(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The fused step's final arriver, each thread before its first write of the packed system: the
-// spare's acknowledgement (ack, loaded with the thread's batch) must be this launch's (want = the
-// spare_seq every workgroup of the launch read + 1).  Polls (sc1 loads) up to LinArgs::spare_wait; the
+// spare's acknowledgement (ack, loaded with the thread's batch) must be this update launch's (want =
+// the iteration every workgroup of the launch read + 1).  Polls (sc1 loads) up to LinArgs::spare_wait; the
 // spare is the grid's last workgroup and the other photos have exited, so it runs unless the device is
 // held by others.  false: gave up (*to = 1; the step fails at the next barrier, spare_failed).
-__device__ __forceinline__ bool spare_wait(const LinArgs& a, unsigned ack, unsigned want, int* to, int* waited) {
+__device__ __forceinline__ bool spare_wait(const LinArgs& a, unsigned ack, unsigned want, int* to) {
     if (ack == want) return true;
-    *waited = 1;
+    if (threadIdx.x == 0 && a.solve.sstats)   // (statistics: a step that waited)
+        atomicAdd(reinterpret_cast<unsigned long long*>(a.solve.sstats + 4), 1ull);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     do {
         __builtin_amdgcn_s_sleep(2);
@@ -1018,7 +1017,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         else if (lane < 8) P.nrm[lane - 6] = a.photo_norm[2 * (size_t)photo + lane - 6];   // k_backsub flush
         else if (lane < 10) P.cn[lane - 8] = lane == 8 ? st->cam_normG2 : st->cam_normX2;
         else if (lane == 10) P.iter0 = st->iter;
-        else if (lane == 11) P.seq0 = st->spare_seq;
         if (pending) {
             if (lane < 6) lov = a.zp[6 * (size_t)photo + lane];   // z' = Hpp^-1 gp
             // lane l < 60: k = l % 6, columns l / 6 + 10 u (m <= 30): sum_col W[k][col] dg[col].
@@ -1431,10 +1429,14 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     // the spare's acknowledgement of this launch (small_inverse): no thread writes the packed system or
     // the state before it has seen it; a thread that gave up (spare_wait's bound) sets ack_to, and the
     // step then fails after the next barrier instead of solving
-    const bool spare = a.ssinv != nullptr;
-    const unsigned want = P.seq0 + 1u;
-    __shared__ int ack_to, ack_waited;
-    if (tid == 0) ack_to = ack_waited = 0;
+#ifdef MCC_NO_SPARE_ACK   // (A/B builds only: the round-4 race, for pricing the acknowledgement)
+    const bool spare = false;
+#else
+    const bool spare = a.ssinv != nullptr;   // (update launches only: enqueue_step)
+#endif
+    const unsigned want = (unsigned)P.iter0 + 1u;   // (update launches only: spare_wait)
+    __shared__ int ack_to;
+    if (tid == 0) ack_to = 0;
     __syncthreads();
     auto place = [&](int t, double v) {
         if (t < ntri) {
@@ -1490,16 +1492,13 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         double v = 0.0;
 #pragma unroll
         for (int q = 0; q < 24; ++q) v += q < ng ? b[q] : 0.0;   // group order (sum_sc1's additions)
-        if (spare_wait(a, ack, want, &ack_to, &ack_waited) && tid < Lc) finish_entry(tid, v, err_now);
-    } else if (spare_wait(a, spare ? ld_agent_u32(&st->spare_ack) : want, want, &ack_to, &ack_waited)) {
+        if (spare_wait(a, ack, want, &ack_to) && tid < Lc) finish_entry(tid, v, err_now);
+    } else if (spare_wait(a, spare ? ld_agent_u32(&st->spare_ack) : want, want, &ack_to)) {
         for (int t = tid; t < Lc; t += blockDim.x) {
             const double v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
             finish_entry(t, v, photo_error(st));
         }
     }
-    // (thread 0 has seen the acknowledgement: the spare read spare_seq before it; the next launch's
-    // photos and spare read the new value)
-    if (spare && tid == 0 && !ack_to) st->spare_seq = want;
     STAMP(17);   // thread 0's share of the assembly done (MCC_DIAG)
     if (peer) {   // multi-GPU: rank-ordered sum of every rank's system, then this rank solves
         if (spare) {
@@ -1522,7 +1521,6 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     }
     __syncthreads();
     if (spare && spare_failed(st, ack_to)) { RSTAMP(15); return; }
-    if (spare && tid == 0 && ack_waited && a.solve.sstats) atomicAdd((unsigned long long*)(a.solve.sstats + 4), 1ull);
     STAMP(12);
     SolveCtx sc = a.solve;
 #ifdef MCC_DIAG
@@ -3214,7 +3212,7 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 // inverts the packed system the previous step's k_schur left (gj_inverse_rows) while the groups
 // linearise; k_schur's final arriver reads it after the kernel boundary.  The fused step (k_linearize)
 // appends the spare to the same launch whose final arriver rewrites the packed system and the state, so
-// there the spare acknowledges (State::spare_ack = spare_seq + 1) once it holds its inputs in LDS, and
+// there the spare acknowledges (State::spare_ack = iteration + 1) once it holds its inputs in LDS, and
 // the final arriver writes neither before it has seen that (spare_wait): the spare always inverts the
 // previous launch's system and tags it with this launch's iteration, however late it is scheduled.
 // Every step forms it, so the branch a step takes -- refinement, or the elimination when there is no
@@ -3236,10 +3234,11 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool 
         __syncthreads();
     }
     // buffer iteration & 1, tagged iteration + 1 (0: none): k_schur of this step reads it, the fused
-    // step's final arriver of the NEXT launch does (this launch's is still inverting)
+    // step's final arriver of the NEXT launch does (this launch's is still inverting).  A fused launch
+    // that updates nothing (linearisation only) has no spare (enqueue_step).
     const int done = st->done, it = st->iter, pend = st->pending;
-    const unsigned seq = st->spare_seq;
-    if (done) return;   // no final arriver waits (the photos see the same word)
+    if (done) return;   // (the photos see the same word)
+    const unsigned seq = (unsigned)it;
     double* out = a.ssinv + (size_t)(it & 1) * m * m;
     int* okp = a.ssinv_ok + (it & 1);
     __shared__ int ok_s;
@@ -3470,6 +3469,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         st->done = 1;
         if (warm) warm_stop(*warm);
     }
+#ifndef MCC_NO_SSTATS   // (A/B builds only)
     if (!LARGE && tid == 64 && a.sstats) {   // m <= 30 warm-solve statistics, last (nothing waits on them)
         unsigned long long* ss = reinterpret_cast<unsigned long long*>(a.sstats);
         if (Iv) {
@@ -3480,6 +3480,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
             atomicAdd(ss + 3, 1ull);
         }
     }
+#endif
 }
 
 // ---------------------------------------------------------------- k_schur

@@ -223,7 +223,8 @@ def test_fused_spare_delayed_is_bitwise_the_undelayed_run(views):
     exits.  Both runs repeat bitwise (a second undelayed run), and refine: every update step after
     the first two has an inverse of the right iteration.  The loop is src/multicalib.cpp:462-514."""
     p = rig.make_config("config2", n_views=views)
-    runs = [_fused_runs(p, env) for env in ({}, {}, {"MCC_SPARE_DELAY_US": "300"})]
+    st = {"MCC_SOLVE_STATS": "1"}   # the m <= 30 counters (off by default: ~0.5 us per step)
+    runs = [_fused_runs(p, dict(st, **env)) for env in ({}, {}, {"MCC_SPARE_DELAY_US": "300"})]
     (x0, it0, xs0, so0, sa0) = runs[0]
     for (x, it, xs, so, sa) in runs[1:]:
         assert it == it0
