@@ -1464,8 +1464,10 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
 #pragma unroll
         for (int u = 0; u < kIvF; ++u) ivv[u] = src[min(u * (int)blockDim.x + tid, m * m - 1)];
     }
-    auto finish_entry = [&](int t, double v, int err) {
-        if (t >= ntri + 2 * m) {   // stop-test norms: photos of every rank + the camera block once
+    // entry t's final value (the stop-test norms: photos of every rank + the camera block once), placed
+    // in the solve's LDS -- the packed system's global copy is written after the spare's acknowledgement
+    auto finish_value = [&](int t, double v, int err) {
+        if (t >= ntri + 2 * m) {
             const int w = t - ntri - 2 * m;
             if (iter0 > 0) {
                 if (a.rank == 0) v += w ? cnX : cnG;
@@ -1475,7 +1477,7 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
             v = photo_flag_norm(err, w, v);
         }
         if (!peer) place(t, v);
-        a.packed[t] = v;
+        return v;
     };
     if (Lc <= (int)blockDim.x && a.n_groups <= 24) {
         // one entry per thread (m <= 18), its column of group sums in one batch of loads with no
@@ -1488,15 +1490,19 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
         // waits for it at once, which in front of the batch would be a memory round trip of its own;
         // the spare's acknowledgement likewise (normally long there: the spare reads its inputs first)
         const int err_now = photo_error(st);
-        const unsigned ack = spare ? ld_agent_u32(&st->spare_ack) : want;
+        // (unconditional: a load under `spare ?` joins the branch with a wait for every load in flight)
+        const unsigned ack = ld_agent_u32(&st->spare_ack);
         double v = 0.0;
 #pragma unroll
         for (int q = 0; q < 24; ++q) v += q < ng ? b[q] : 0.0;   // group order (sum_sc1's additions)
-        if (spare_wait(a, ack, want, &ack_to) && tid < Lc) finish_entry(tid, v, err_now);
+        if (tid < Lc) v = finish_value(tid, v, err_now);
+        // the acknowledgement, loaded with the batch, is tested only now: ahead of the sums its compare
+        // held them until every load had landed (+0.4 us per config2 step)
+        if (spare_wait(a, spare ? ack : want, want, &ack_to) && tid < Lc) a.packed[tid] = v;
     } else if (spare_wait(a, spare ? ld_agent_u32(&st->spare_ack) : want, want, &ack_to)) {
         for (int t = tid; t < Lc; t += blockDim.x) {
             const double v = sum_sc1(a.gsum + t, a.n_groups, Lcp);
-            finish_entry(t, v, photo_error(st));
+            a.packed[t] = finish_value(t, v, photo_error(st));
         }
     }
     STAMP(17);   // thread 0's share of the assembly done (MCC_DIAG)
