@@ -228,6 +228,13 @@ struct mcc_problem {
     long long warm_wait_ticks = 1000000000LL, warm_idle_ticks = 4000000000LL, warm_delay_ticks = 0;
     long long spare_delay_ticks = 0;  // MCC_SPARE_DELAY_US (test): the fused step's spare starts this late
     bool small_stats = false;         // MCC_SOLVE_STATS=1: count the m <= 30 warm solves (SolveCtx::sstats)
+    // k_group's step with k_schur's reduction and the solve folded into the same launch (LinArgs::fold;
+    // MCC_GFOLD=0 keeps k_group -> k_schur): fnorm [4V] and fiv [m^2 + 1] hand-off words, kFoldEmpty
+    // between launches like the slots and the item partials
+    bool gfold = false;
+    int fold_direct = 0;   // the final workgroup sums where the words land (LinArgs::fold_direct)
+    int max_item_slots = 0;
+    DevBuf<double> fnorm, fiv;
     int fault_photo = -1;            // MCC_FAULT_PHOTO (test): LinArgs::fault_photo
     DevBuf<unsigned char> edge_lphoto;
     DevBuf<unsigned> gcon;
@@ -391,6 +398,46 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
     la.solve.stamps = nullptr;
     la.n_edges = p->E; la.n_photos = p->V;
     la.erec = p->erec.p; la.echain = p->echain.p; la.eh = p->eh.p;
+    SchurArgs sa{};
+    // m > 30: the register-tiled elimination runs in its own kernel (k_solve); with RCCL the
+    // all-reduce sits between the reduction and k_solve; with the peer transport and m <= 30, the
+    // reduction's final workgroup exchanges and solves (no k_peer_push / k_solve launches)
+    const bool split = rccl || p->m > 30;
+    if (!p->fused) {
+        sa.state = p->state.p;
+        sa.items = p->items.p;
+        sa.pairprod = p->pairprod.p;
+        sa.item_out = p->item_out.p;
+        sa.n_items = p->n_items;
+        sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
+        sa.counter = p->counter.p;
+        sa.cnt_blk = p->cnt_blk.p;
+        sa.nblk = p->nblk;
+        sa.block_items = p->block_items.p;
+        sa.packed = p->packed.p;
+        sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
+        sa.one_level = p->schur_one_level;
+        sa.prev2 = p->warm && do_update && !p->comm && !p->peer_on ? p->prev2 : nullptr;   // single GPU
+        sa.prev_stride = p->prev_stride;
+        sa.ssinv = swarm ? p->ssinv.p : nullptr;
+        sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
+        sa.peer = peer_ctx(p, peer && !split);
+        sa.solve = solve_ctx(p, do_update);
+        sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
+    }
+    // k_group's step as one launch (LinArgs::fold): the reduction's workgroups follow the groups; the
+    // timing probe's linearisation-only launches run k_group alone and empty the slots after it
+    const bool fold = p->gfold && !lin_only;
+    if (fold) {
+        la.fold = 1;
+        la.fold_parts = p->n_items + p->n_norm_chunks;
+        la.fold_direct = p->fold_direct;
+        la.fsa = sa;
+        la.fsa.ssinv = la.ssinv ? p->fiv.p : nullptr;   // this launch's spare -> the final workgroup
+        la.fsa.ssinv_ok = nullptr;
+        la.fnorm = p->fnorm.p;
+        la.fiv = p->fiv.p;
+    }
     if (p->V > 0) {
         if (!p->fused && p->use_group)
             HIPCHK(mcc_launch_group(la, p->model, p->rational, p->prism, p->group_lanes, p->group_shmem, p->stream));
@@ -422,32 +469,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
         return MCC_OK;
     }
 
-    SchurArgs sa{};
-    sa.state = p->state.p;
-    sa.items = p->items.p;
-    sa.pairprod = p->pairprod.p;
-    sa.item_out = p->item_out.p;
-    sa.n_items = p->n_items;
-    sa.photo_norm = p->photo_norm.p; sa.n_photos = p->V;
-    sa.counter = p->counter.p;
-    sa.cnt_blk = p->cnt_blk.p;
-    sa.nblk = p->nblk;
-    sa.block_items = p->block_items.p;
-    sa.packed = p->packed.p;
-    // m > 30: the register-tiled elimination runs in its own kernel (k_solve); with RCCL the
-    // all-reduce sits between k_schur and k_solve; with the peer transport and m <= 30, k_schur's
-    // final arriver exchanges and solves (no k_peer_push / k_solve launches)
-    const bool split = rccl || p->m > 30;
-    sa.m = p->m; sa.rank = p->rank; sa.fuse_solve = split ? 0 : 1;
-    sa.one_level = p->schur_one_level;
-    sa.prev2 = p->warm && do_update && !p->comm && !p->peer_on ? p->prev2 : nullptr;   // single GPU
-    sa.prev_stride = p->prev_stride;
-    sa.ssinv = swarm ? p->ssinv.p : nullptr;
-    sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
-    sa.peer = peer_ctx(p, peer && !split);
-    sa.solve = solve_ctx(p, do_update);
-    sa.stamps = p->stamps.p ? p->stamps.p + mcc::kStampStride * (size_t)std::max(p->V, 1) : nullptr;
-    HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
+    if (!fold) HIPCHK(mcc_launch_schur(sa, p->n_items + p->n_norm_chunks, p->stream));
     if (rccl) {
         const bool tx = tim && p->ev_x_used + 2 <= (int)p->ev_x.size();
         if (tx) HIPCHK(hipEventRecord(p->ev_x[p->ev_x_used], p->stream));
@@ -866,9 +888,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         int per_item = std::max(min_slots, (nsl + 23) / 24);
         if (nsl > single_max && nsl <= per_item) per_item = (nsl + 1) / 2;
         const int single = (nsl <= per_item) ? mcc::kItemSingle : 0;
-        for (int s = begin; s < end; s += per_item)
+        for (int s = begin; s < end; s += per_item) {
             items.push_back(make_int4(b, (int)(base + (size_t)(s - begin) * stride), std::min(end, s + per_item) - s,
                                       stride | single));
+            p->max_item_slots = std::max(p->max_item_slots, items.back().z);
+        }
         // a block no photo couples gets one empty item: it writes the block's zeros (every packed
         // entry is rewritten each step; the all-reduce leaves sums there)
         if (begin == end) items.push_back(make_int4(b, (int)base, 0, stride | mcc::kItemSingle));
@@ -1036,6 +1060,29 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
             HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
         }
     }
+    // the folded reduction: k_group's one-level m <= 30 step with items of at most kSub x kFoldSlots
+    // slots (every m <= 30 rig with several camera-pair blocks takes 64; a one-block rig 320: no fold)
+    p->gfold = !p->fused && p->use_group && p->schur_one_level && p->max_item_slots <= 5 * 13 &&
+               48 * (p->n_items + p->n_norm_chunks) + p->m * p->m + 1 <= mcc::kSchurOneLevelLoads * 256;
+    if (const char* f = std::getenv("MCC_GFOLD")) p->gfold = p->gfold && std::atoi(f) != 0;
+    if (p->gfold) {
+        // the final workgroup's LDS (k_schur's one-level layout) within k_group's
+        const size_t fs = mcc::schur_lds_bytes(p->m, 1, 1, 1, p->n_items + p->n_norm_chunks, p->nblk);
+        if (fs > p->group_shmem) {
+            p->group_shmem = fs;
+            HIPC(mcc_set_kernel_attrs(p->max_epp, C, p->m, p->max_cpp, p->photo_shmem, p->group_shmem));
+        }
+        HIPC(p->fnorm.alloc(4 * (size_t)std::max(V, 1)));
+        HIPC(p->fiv.alloc((size_t)p->m * p->m + 1));
+        int max_bi = 0;
+        for (int b = 0; b < p->nblk; ++b) max_bi = std::max(max_bi, block_items[b + 1] - block_items[b]);
+        const int ivt = 512 - 48 * p->nblk - 2;   // the inverse's threads
+        p->fold_direct = p->group_lanes == 32 && max_bi <= 8 && p->n_norm_chunks <= 4 && ivt > 0 &&
+                         p->m * p->m <= 8 * ivt;
+        if (const char* f = std::getenv("MCC_FOLD_DIRECT")) p->fold_direct = p->fold_direct && std::atoi(f) != 0;
+        for (auto* b : {&p->pairprod, &p->item_out, &p->fnorm, &p->fiv})
+            if (b->p) HIPC(hipMemset(b->p, 0xFF, sizeof(double) * std::max<size_t>(b->n, 1)));
+    }
     p->warm = !p->fused && p->m > 30;
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
@@ -1093,7 +1140,7 @@ void mcc_destroy(mcc_problem* p) {
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->corner_err.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
-    p->erec.release(); p->echain.release(); p->eh.release(); p->tilt.release(); p->ssinv.release(); p->ssinv_ok.release();
+    p->erec.release(); p->echain.release(); p->eh.release(); p->tilt.release(); p->fnorm.release(); p->fiv.release(); p->ssinv.release(); p->ssinv_ok.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();
@@ -1491,6 +1538,9 @@ int mcc_timing_linearize(mcc_problem* p, int launches, double* ms_per_launch) {
     HIPCHK(hipMemcpyAsync(p->x.p, p->xsave.p, sizeof(float) * p->P, hipMemcpyDeviceToDevice, p->stream));
     HIPCHK(hipMemcpyAsync(p->Y.p, p->ysave.p, sizeof(double) * p->Y.n, hipMemcpyDeviceToDevice, p->stream));
     HIPCHK(hipMemcpyAsync(p->zp.p, p->zpsave.p, sizeof(double) * p->zp.n, hipMemcpyDeviceToDevice, p->stream));
+    // the folded step's slots are empty between launches (LinArgs::fold): the probe's k_group alone
+    // wrote them with nothing to consume them
+    if (p->gfold) HIPCHK(hipMemsetAsync(p->pairprod.p, 0xFF, sizeof(double) * p->pairprod.n, p->stream));
     HIPCHK(hipStreamSynchronize(p->stream));
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, p->ev_win[0], p->ev_win[1]));

@@ -288,6 +288,387 @@ __device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, i
     }
 }
 
+// ---------------------------------------------------------------- the folded reduction (gfold)
+// k_group's step with k_schur's one-level reduction and the m <= 30 solve in the SAME launch
+// (LinArgs::fold): after the groups (and the spare) the grid holds one item
+// workgroup per k_schur item, one per norm chunk, and a final workgroup.  Nothing signals: every
+// handed-off word is its own flag (kFoldEmpty until the producer's 8-byte sc1 store lands; 8-byte
+// aligned halves of a store are single-copy atomic), each consumer polls the words it needs with sc1
+// loads and writes kFoldEmpty back once it has read them, so the words are empty again before the next
+// launch's producers (after the kernel boundary).  A consumer waits only on workgroups with lower grid
+// indices, which are dispatched before it, so the grid needs no co-residency.  The sums are k_schur's,
+// in its order (kSub sub-chunks per item entry, chunks in photo order, items in item order), so the
+// bits are the k_group -> k_schur step's.  Where k_schur's boundary and item phase followed the last
+// group (~4 us at config4), the items here have summed most slots by then.
+__device__ __forceinline__ bool fold_valid(double v) { return __double_as_longlong(v) != kFoldEmpty; }
+__device__ __forceinline__ void fold_empty(double* p) { st_sc1(p, __longlong_as_double(kFoldEmpty)); }
+// a poll that outlives LinArgs::spare_wait: the step fails (MCC_ETIMEOUT) and the loop stops
+__device__ __forceinline__ bool fold_timed_out(const LinArgs& a, long long t0) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 < a.spare_wait) return false;
+    atomicOr(&a.state->error, kErrWarmTimeout);
+    a.state->done = 1;
+    return true;
+}
+
+// item workgroup: the item's slots (sub-chunk sub sums slots sub, sub + kSub, ... of entry q, k_schur's
+// order), each thread loading all of its slots in one batch and adding the valid prefix in order; the
+// item's 48-entry partial -> fsa.item_out (sc1)
+constexpr int kFoldSlots = 13;   // slots per thread: items of <= 64 slots (mcc_create) over kSub sub-chunks
+__device__ __forceinline__ void fold_item(const LinArgs& la, int item) {
+    const SchurArgs& a = la.fsa;
+    const int tid = threadIdx.x;
+    const int4 it = a.items[item];   // {block, first slot's offset (doubles), slots, slot size 48 | 36}
+    const int q = tid % 48, sub = tid / 48, sz = it.w & (kItemSingle - 1);
+    __shared__ double part[kSub][48];
+    __shared__ int fail;
+    long long* srow = a.stamps ? a.stamps + kSchurStampStride * (size_t)item : nullptr;   // MCC_DIAG
+    SSTAMP(srow, 0, 0);
+    if (tid == 0) fail = 0;
+    double s = 0.0;
+    const int ns = sub < kSub ? (it.z - sub + kSub - 1) / kSub : 0;   // this thread's slots
+    if (ns > 0 && q < sz) {
+        const double* pp = a.pairprod + (size_t)it.y + q;
+        int next = 0;
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            double v[kFoldSlots];
+#pragma unroll
+            for (int u = 0; u < kFoldSlots; ++u) v[u] = ld_sc1(pp + (size_t)sz * (sub + kSub * min(u, ns - 1)));
+#pragma unroll
+            for (int u = 0; u < kFoldSlots; ++u)
+                if (u == next && u < ns && fold_valid(v[u])) {
+                    s += v[u];
+                    ++next;
+                }
+            if (next >= ns) break;
+            if (fold_timed_out(la, t0)) { fail = 1; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s += 0.0;   // (k_schur adds its batch's zero padding: -0.0 becomes +0.0 there too)
+        for (int u = 0; u < ns; ++u) fold_empty(const_cast<double*>(pp) + (size_t)sz * (sub + kSub * u));
+    }
+    if (sub < kSub) part[sub][q] = s;
+    __syncthreads();
+    if (tid < 48 && !fail) {
+        double t = part[0][tid];
+        for (int c = 1; c < kSub; ++c) t += part[c][tid];
+        st_sc1(a.item_out + 48 * (size_t)item + tid, t);
+    }
+    SSTAMP(srow, 1, 0);
+}
+
+// norm-chunk workgroup c: 256 photos' ||G||^2, ||x||^2 (k_schur's norm chunk: a fixed butterfly per
+// wave, the four waves in order) and their not-PD flags (the final workgroup's photo error)
+__device__ __forceinline__ void fold_chunk(const LinArgs& la, int c) {
+    const SchurArgs& a = la.fsa;
+    const int tid = threadIdx.x;
+    __shared__ double wred[3][kSchurThreads / 64];
+    __shared__ int fail;
+    long long* srow = a.stamps ? a.stamps + kSchurStampStride * (size_t)(a.n_items + c) : nullptr;   // MCC_DIAG
+    SSTAMP(srow, 0, 0);
+    if (tid == 0) fail = 0;
+    if (tid < kSchurThreads) {   // waves 0..3
+        const int p = c * kSchurThreads + tid;
+        double g = 0.0, x = 0.0, bad = 0.0;
+        if (p < a.n_photos) {
+            const double* fp = la.fnorm + 4 * (size_t)p;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            for (;;) {
+                const double w0 = ld_sc1(fp), w1 = ld_sc1(fp + 1), w2 = ld_sc1(fp + 2);
+                if (fold_valid(w0) && fold_valid(w1) && fold_valid(w2)) {
+                    g = w0; x = w1; bad = w2;
+                    break;
+                }
+                if (fold_timed_out(la, t0)) { fail = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            double* fw = la.fnorm + 4 * (size_t)p;
+            fold_empty(fw); fold_empty(fw + 1); fold_empty(fw + 2);
+        }
+        g = wave_sum(g);
+        x = wave_sum(x);
+        bad = wave_sum(bad);
+        if ((tid & 63) == 0) {
+            wred[0][tid >> 6] = g;
+            wred[1][tid >> 6] = x;
+            wred[2][tid >> 6] = bad;
+        }
+    }
+    __syncthreads();
+    if (tid < 3 && !fail) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < kSchurThreads / 64; ++w) v += wred[tid][w];
+        st_sc1(a.item_out + 48 * (size_t)(a.n_items + c) + tid, v);
+    }
+    SSTAMP(srow, 1, 0);
+}
+
+// the final workgroup: every partial (48 per item / chunk) and the spare's inverse with its status into
+// LDS by polling (each thread a fixed set of words, re-read until valid; the inverse's words only when
+// the status says there is one), then kFoldEmpty back into all of them, and k_schur's one-level finish
+// (sums in item order, placement, the refinement or elimination, the camera update)
+template <int U>
+__device__ __forceinline__ void fold_final_u(const LinArgs& la) {
+    const SchurArgs& a = la.fsa;
+    State* st = a.state;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int m = a.m, np = la.fold_parts;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const bool useiv = a.ssinv != nullptr && a.fuse_solve;   // (a.ssinv is la.fiv here)
+    double* Iv = sm + m * m + m;
+    double* itm = sm + schur_items_offset(m, a.fuse_solve, a.ssinv != nullptr);   // [np][48]
+    int* sbi = reinterpret_cast<int*>(itm + 48 * (size_t)np);                       // [nblk + 1]
+    __shared__ double s_status;
+    __shared__ int s_fail;
+    long long* srow = a.stamps ? a.stamps + kSchurStampStride * (size_t)np : nullptr;   // MCC_DIAG: after the parts
+    SSTAMP(srow, 10, 0);   // (slots 0..2 are the solve's)
+    const int bi = a.block_items[tid < a.nblk ? tid : a.nblk];
+    const int iter = st->iter;
+    const double cn0 = st->cam_normG2, cn1 = st->cam_normX2;
+    const int nI = 48 * np, nV = useiv ? m * m + 1 : 0, n = nI + nV;
+    if (tid == 0) {
+        s_status = useiv ? 0.0 : -1.0;   // 0: not seen yet; no inverse buffer: none
+        s_fail = 0;
+    }
+    __syncthreads();
+    unsigned have = 0;   // words of this thread already in LDS
+    // (a norm chunk's partial carries 3 words: ||G||^2, ||x||^2, the not-PD count; an item's all 48)
+    auto due = [&](int t) { return t >= nI || t < 48 * a.n_items || t % 48 < 3; };
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int t = u * nt + tid;
+            t = t < n ? t : n - 1;
+            v[u] = ld_sc1(t < nI ? a.item_out + t : la.fiv + (t - nI));
+        }
+        // (every thread reads the status itself: its inverse words are due unless it says "none")
+        const double stt = useiv ? ld_sc1(la.fiv + m * m) : -1.0;
+        int pend = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int t = u * nt + tid;
+            if (t >= n || ((have >> u) & 1) || !due(t)) continue;
+            if (!fold_valid(v[u])) {
+                // partials and the status are always due; the inverse unless the status says "none"
+                if (t < nI || t == nI + m * m || !fold_valid(stt) || stt > 0.0) ++pend;
+                continue;
+            }
+            have |= 1u << u;
+            if (t < nI) itm[t] = v[u];
+            else if (t < nI + m * m) Iv[t - nI] = v[u];
+            else s_status = v[u];
+        }
+        if (!__syncthreads_or(pend)) break;
+        // the poll bound, decided by one thread for all (the loop's barriers stay matched)
+        if (tid == 0 && (long long)__builtin_amdgcn_s_memrealtime() - t0 >= la.spare_wait) {
+            atomicOr(&st->error, kErrWarmTimeout);
+            st->done = 1;
+            s_fail = 1;
+        }
+        __syncthreads();
+        if (s_fail) return;
+    }
+    // every word back to kFoldEmpty for the next launch's producers (this launch's have all landed)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int t = u * nt + tid;
+        if (t < n && ((have >> u) & 1)) fold_empty(t < nI ? a.item_out + t : la.fiv + (t - nI));
+    }
+    if (tid <= a.nblk) sbi[tid] = bi;
+    // a photo block that is not positive definite (any chunk's flag sum, entry 2)
+    int err_now = 0;
+    for (int k = a.n_items; k < np; ++k) err_now |= itm[48 * k + 2] != 0.0 ? kErrPhotoNotPD : 0;
+    __syncthreads();
+    SSTAMP(srow, 8, 0);   // the partials landed in LDS
+    schur_finish(a, np, iter, cn0, cn1, err_now, useiv && s_status > 0, srow);
+}
+// The final workgroup with the sums formed where the words land (LinArgs::fold_direct: 512 threads,
+// <= 8 items per camera-pair block, <= 4 norm chunks -- config4): thread t < 48 nblk owns entry t of
+// the packed system and polls its block's item words straight into registers, adding them in item
+// order (k_schur's order, so the same bits); threads 48 nblk, +1 own ||G||^2, ||x||^2 (each with the
+// chunks' not-PD counts), the rest the spare's inverse.  Nothing passes through an LDS copy of the
+// partials: the copy, a barrier and the runtime-bounded LDS sums (~1.8 us from the landed batch to the
+// placed sums at config4) leave the tail.
+constexpr int kFoldKI = 8;   // words per thread
+__device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
+    const SchurArgs& a = la.fsa;
+    State* st = a.state;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2, np = la.fold_parts, nc = np - a.n_items;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* S = sm;
+    double* r = sm + m * m;
+    double* Iv = sm + m * m + m;
+    __shared__ double norms[2];
+    __shared__ int s_fail;
+    const bool useiv = a.ssinv != nullptr && a.fuse_solve;
+    const bool lds = a.fuse_solve && a.peer.nranks == 0;
+    long long* srow = a.stamps ? a.stamps + kSchurStampStride * (size_t)np : nullptr;   // MCC_DIAG
+    SSTAMP(srow, 10, 0);
+    const int nent = a.nblk * 48, ivt0 = nent + 2, nivt = nt - ivt0;
+    // this thread's words
+    const double* src[kFoldKI];
+    int cnt = 0, kind = 0;   // kind 1: an entry, 2: a norm (+ not-PD counts), 3: inverse words
+    int blk = 0, e = 0;
+    if (tid < nent) {
+        blk = tid / 48;
+        e = tid % 48;
+        const int k0 = a.block_items[blk], nk = a.block_items[blk + 1] - k0;
+        int b1 = 0;
+#pragma unroll
+        for (int b = 1; b < 5; ++b)
+            if (b < nb && b * nb - b * (b - 1) / 2 <= blk) b1 = b;
+        const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
+        kind = 1;
+        cnt = e >= 36 && b1 != b2 ? 0 : nk;   // (off-diagonal blocks: 36 entries)
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) src[q] = a.item_out + 48 * (size_t)(k0 + (q < nk ? q : 0)) + e;
+    } else if (tid < ivt0) {
+        const int w = tid - nent;
+        kind = 2;
+        cnt = 2 * nc;   // chunk words w, then the chunks' not-PD counts (entry 2)
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) {
+            const int c = q < nc ? q : (q - nc < nc ? q - nc : 0);
+            src[q] = a.item_out + 48 * (size_t)(a.n_items + c) + (q < nc ? w : 2);
+        }
+    } else {
+        kind = 3;
+        const int j0 = tid - ivt0;
+        cnt = 0;
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) {
+            const int j = j0 + q * nivt;
+            if (useiv && j < m * m) cnt = q + 1;
+            src[q] = la.fiv + (useiv && j < m * m ? j : 0);
+        }
+    }
+    // the state words, read ahead of the poll (their loads overlap it)
+    const int iter = st->iter;
+    const double cn = kind == 2 && a.rank == 0 ? (tid - nent ? st->cam_normX2 : st->cam_normG2) : 0.0;
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    double kv[kFoldKI];
+    unsigned have = 0;
+    double stt = -1.0;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        double v[kFoldKI];
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) v[q] = ld_sc1(src[q]);
+        if (useiv) stt = ld_sc1(la.fiv + m * m);
+        int pend = tid == 0 && useiv && !fold_valid(stt) ? 1 : 0;
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) {
+            if (q >= cnt || ((have >> q) & 1)) continue;
+            if (fold_valid(v[q])) {
+                kv[q] = v[q];
+                have |= 1u << q;
+            } else if (kind != 3 || !fold_valid(stt) || stt > 0.0) {
+                ++pend;   // the inverse's words are due unless the status says "none"
+            }
+        }
+        if (!__syncthreads_or(pend)) break;
+        if (tid == 0 && (long long)__builtin_amdgcn_s_memrealtime() - t0 >= la.spare_wait) {
+            atomicOr(&st->error, kErrWarmTimeout);
+            st->done = 1;
+            s_fail = 1;
+        }
+        __syncthreads();
+        if (s_fail) return;
+    }
+    SSTAMP(srow, 8, 0);   // every word landed
+    const bool ivok = useiv && stt > 0.0;
+    // every word back to kFoldEmpty for the next launch's producers
+#pragma unroll
+    for (int q = 0; q < kFoldKI; ++q)
+        if ((have >> q) & 1) fold_empty(const_cast<double*>(src[q]));
+    if (tid == 0 && useiv) fold_empty(la.fiv + m * m);
+    if (kind == 1 && cnt > 0) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q)
+            if (q < cnt) v += kv[q];   // item order (k_schur's level-1 sums)
+        int b1 = 0;
+#pragma unroll
+        for (int b = 1; b < 5; ++b)
+            if (b < nb && b * nb - b * (b - 1) / 2 <= blk) b1 = b;
+        const int b2 = b1 + (blk - (b1 * nb - b1 * (b1 - 1) / 2));
+        if (e < 36) {
+            const int ii = e / 6, jj = e % 6, i = 6 * b1 + ii, j = 6 * b2 + jj;
+            if (b1 != b2 || ii <= jj) {
+                a.packed[packed_index(i, j, m)] = v;
+                if (lds) {
+                    S[i * m + j] = v;
+                    S[j * m + i] = v;
+                }
+            }
+        } else {
+            const int w = (e - 36) / 6, i = 6 * b1 + (e - 36) % 6;
+            a.packed[ntri + w * m + i] = v;   // r (w = 0), JTE of the global block (w = 1)
+            if (lds && w == 0) r[i] = v;
+        }
+    } else if (kind == 2) {
+        const int w = tid - nent;
+        double nrm = 0.0, bad = 0.0;
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q) {
+            if (q < nc) nrm += kv[q];                  // chunk order
+            else if (q < 2 * nc) bad += kv[q];
+        }
+        if (a.rank == 0) nrm += cn;
+        if (iter <= 0) nrm = 0.0;
+        nrm = photo_flag_norm(bad != 0.0 ? kErrPhotoNotPD : 0, w, nrm);
+        norms[w] = nrm;
+        a.packed[ntri + 2 * m + w] = nrm;
+    } else if (kind == 3 && ivok) {
+        const int j0 = tid - ivt0;
+#pragma unroll
+        for (int q = 0; q < kFoldKI; ++q)
+            if (q < cnt) Iv[j0 + q * nivt] = kv[q];
+    }
+    SSTAMP(srow, 9, 0);   // sums placed (thread 0)
+    if (!a.fuse_solve) return;
+    __syncthreads();   // S, r, the inverse and the norms in LDS
+    if (a.peer.nranks > 0) {
+        if (!peer_exchange(a.peer, st, a.packed)) return;
+        for (int t = tid; t < ntri + m; t += nt) {
+            const double v = a.packed[t];
+            if (t < ntri) {
+                int i, j;
+                packed_ij(t, m, i, j);
+                S[i * m + j] = v;
+                S[j * m + i] = v;
+            } else {
+                r[t - ntri] = v;
+            }
+        }
+        if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
+        __syncthreads();
+    }
+    SSTAMP(srow, 3, 0);
+    SolveCtx sc = a.solve;
+    sc.stamps = srow;
+    solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, ivok ? Iv : nullptr);
+    SSTAMP(srow, 7, 0);
+}
+// (one batch width per k_group shape: the host keeps 48 parts + m^2 + 1 within k_schur's one-level
+// bound, kSchurOneLevelLoads x 256 words)
+template <int NT>
+__device__ __forceinline__ void fold_final(const LinArgs& la) {
+    if (NT == 512 && la.fold_direct) {
+        fold_final_direct(la);
+        return;
+    }
+    constexpr int UM = kSchurOneLevelLoads * 256 / NT;
+    const int n = 48 * la.fold_parts + (la.fsa.ssinv != nullptr ? la.fsa.m * la.fsa.m + 1 : 0);
+    if (n <= UM / 2 * NT) fold_final_u<UM / 2>(la);
+    else fold_final_u<UM>(la);
+}
+
 #ifndef MCC_GROUP_PAIR_THREADS
 #define MCC_GROUP_PAIR_THREADS 256   // threads the pair tasks may spread over (config4, 32 lanes: 256 29.0 vs 512 29.8 us per step)
 #endif
@@ -300,9 +681,17 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
+    if (a.ssinv && grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
         extern __shared__ __attribute__((aligned(16))) double smem_spare[];
         small_inverse(a, smem_spare, false);
+        return;
+    }
+    if (a.fold && grp > a.n_pgroups - (a.ssinv ? 0 : 1)) {   // the folded reduction's workgroups
+        if (st->done) return;
+        const int k = grp - a.n_pgroups - (a.ssinv ? 1 : 0);
+        if (k < a.fsa.n_items) fold_item(a, k);
+        else if (k < a.fold_parts) fold_chunk(a, k - a.fsa.n_items);
+        else fold_final<NT>(a);
         return;
     }
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
@@ -431,9 +820,11 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     double zk = 0.0;
     const int pq = (tid - 192) / 6, pk = (tid - 192) % 6;
     const bool ptask = tid >= 192 && pq < np;
+    double2 pn0 = make_double2(0.0, 0.0);   // the fold without a pending update: the norms k_backsub left
     if (ptask) {
         xo = a.x[m + 6 * (size_t)(p0 + pq) + pk];
         if (pending) zk = a.zp[6 * (size_t)(p0 + pq) + pk];
+        else if (a.fold && pk == 0) pn0 = *reinterpret_cast<const double2*>(a.photo_norm + 2 * (size_t)(p0 + pq));
     }
     double y0[6];
     int gb0 = -1;
@@ -516,6 +907,11 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
             }
             a.photo_norm[2 * (size_t)(p0 + pq)] = g2;
             a.photo_norm[2 * (size_t)(p0 + pq) + 1] = x2;
+            pn0 = make_double2(g2, x2);
+        }
+        if (a.fold) {   // (sxn's pad words) the folded norm chunk's input, written after the Cholesky
+            sxn[16 * pq + 6] = pn0.x;
+            sxn[16 * pq + 7] = pn0.y;
         }
         const double om1[3] = {xs[0], xs[1], xs[2]};
         Rot r1;
@@ -720,6 +1116,11 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
 #pragma unroll
         for (int k = 0; k < 18; ++k) L2[k] = make_double2(Li[(2 * k) / 6][(2 * k) % 6], Li[(2 * k + 1) / 6][(2 * k + 1) % 6]);
         if (bad || photo == a.fault_photo) atomicOr(&st->error, kErrPhotoNotPD);
+        if (a.fold) {   // the norm chunk's input: ||G||^2, ||x||^2 and the not-PD flag (sc1, each word its flag)
+            double* fw = a.fnorm + 4 * (size_t)photo;
+            st_sc1_x2(fw, sxn[16 * q + 6], sxn[16 * q + 7]);
+            st_sc1(fw + 2, bad || photo == a.fault_photo ? 1.0 : 0.0);
+        }
     }
     __syncthreads();
     SSTAMP(stp, 8, 0);
@@ -807,14 +1208,23 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
             racc += __shfl_xor(racc, o);
             jacc += __shfl_xor(jacc, o);
         }
-        if (h == 0) {
+        if (h == 0) {   // write-through (sc1): the folded items poll these words in this launch
             double* out = a.pairprod + (size_t)pqv.w;
+#ifdef MCC_SLOT_PLAIN   // (A/B builds only)
 #pragma unroll
             for (int j = 0; j < 6; ++j) out[i0 * 6 + j] = acc[j];
             if (diag) {
                 out[36 + i0] = racc;
                 out[42 + i0] = jacc;
             }
+#else
+#pragma unroll
+            for (int j = 0; j < 6; j += 2) st_sc1_x2(out + i0 * 6 + j, acc[j], acc[j + 1]);
+            if (diag) {
+                st_sc1(out + 36 + i0, racc);
+                st_sc1(out + 42 + i0, jacc);
+            }
+#endif
         }
     }
 #ifdef MCC_DIAG
@@ -884,9 +1294,11 @@ __global__ __launch_bounds__(64, MCC_PREP4_WAVES) void k_prep4(LinArgs a) {
     const bool ptask = pq < np;
     float xo = 0.f;
     double zk = 0.0;
+    double2 pn0 = make_double2(0.0, 0.0);   // the fold without a pending update: the norms k_backsub left
     if (ptask) {
         xo = a.x[m + 6 * (size_t)(p0 + pq) + pk];
         if (pending) zk = a.zp[6 * (size_t)(p0 + pq) + pk];
+        else if (a.fold && pk == 0) pn0 = *reinterpret_cast<const double2*>(a.photo_norm + 2 * (size_t)(p0 + pq));
     }
     double y0[6];
     int gb0 = -1;

@@ -67,6 +67,29 @@ struct SolveCtx {
     long long* sstats;
 };
 
+struct SchurArgs {
+    State* state;
+    const int4* items;   // {camera-pair block, first slot's offset in doubles, slot count, slot size 48 | 36}
+    const double* pairprod;   // 48 (diagonal block) or 36 doubles per slot, written by k_photo, block-major
+    double* item_out;    // [48 * (items + norm chunks)]
+    int n_items;
+    const double* photo_norm; int n_photos;
+    int* counter;        // level-2 ticket over blocks + norm chunks (zero between launches)
+    int* cnt_blk;        // [nblk] level-1 tickets: the last item of a camera-pair block sums it
+    int nblk;
+    const int* block_items;   // [nblk + 1]
+    double* packed;
+    int m, rank, fuse_solve;
+    int one_level;       // m <= 30: one hand-off level (schur_one_level) instead of items -> blocks -> norms
+    const double* ssinv; // m <= 30 warm solve: [2][m x m], this step's in buffer iteration & 1 (k_group's spare)
+    const int* ssinv_ok; // [2] tags (iteration + 1)
+    SolveCtx solve;
+    long long* stamps;   // MCC_DIAG builds: [8 * grid]
+    PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
+    double* prev2;       // m > 30 warm solve: [2][prev_stride] copy of [S | r] for the helper (null: off)
+    int prev_stride;
+};
+
 struct LinArgs {
     State* state;
     const int* photo_ptr;     // [V+1] photo-major edge ranges
@@ -132,7 +155,19 @@ struct LinArgs {
     // the fused step's spare: its wait bound at the final arriver (s_memrealtime ticks; past it the
     // step fails with kErrWarmTimeout), and a test delay before it reads anything (MCC_SPARE_DELAY_US)
     long long spare_wait, spare_delay;
+    // k_group with the step's reduction and solve folded into the same launch (gfold: m <= 30, one
+    // hand-off level): after the groups (and the spare) the grid holds fsa.n_items item workgroups,
+    // the norm chunks (fold_parts in all) and one final workgroup.  The hand-off words are their own
+    // flags: every slot, norm partial, item partial and the spare's inverse holds kFoldEmpty (all-ones,
+    // a NaN no arithmetic produces) until its producer's sc1 store lands, and its consumer puts
+    // kFoldEmpty back after reading it -- no store drain, ticket or fence on either side.
+    int fold, fold_parts;
+    int fold_direct;          // the final workgroup sums where the words land (fold_final_direct)
+    SchurArgs fsa;            // the reduction (k_schur's arguments: items, slots, partials, packed, solve)
+    double* fnorm;            // [4V] per photo ||G||^2, ||x||^2, not-PD flag, pad (the norm chunks' input)
+    double* fiv;              // [m^2 + 1] the spare's inverse and its status, +-(iteration + 1) as a double
 };
+constexpr long long kFoldEmpty = -1LL;
 
 constexpr int kItemSingle = 256;   // k_schur item flag (in .w, over the slot size): the block's only item
 constexpr int kPhotoGroup = 8;        // photos per k_photo workgroup, at most
@@ -239,28 +274,7 @@ __host__ __device__ inline size_t schur_lds_bytes(int m, int fuse, int ssinv, in
 // kSchurOneLevelLoads x 256 (k_schur's threads)
 constexpr int kSchurOneLevelLoads = 16;
 
-struct SchurArgs {
-    State* state;
-    const int4* items;   // {camera-pair block, first slot's offset in doubles, slot count, slot size 48 | 36}
-    const double* pairprod;   // 48 (diagonal block) or 36 doubles per slot, written by k_photo, block-major
-    double* item_out;    // [48 * (items + norm chunks)]
-    int n_items;
-    const double* photo_norm; int n_photos;
-    int* counter;        // level-2 ticket over blocks + norm chunks (zero between launches)
-    int* cnt_blk;        // [nblk] level-1 tickets: the last item of a camera-pair block sums it
-    int nblk;
-    const int* block_items;   // [nblk + 1]
-    double* packed;
-    int m, rank, fuse_solve;
-    int one_level;       // m <= 30: one hand-off level (schur_one_level) instead of items -> blocks -> norms
-    const double* ssinv; // m <= 30 warm solve: [2][m x m], this step's in buffer iteration & 1 (k_group's spare)
-    const int* ssinv_ok; // [2] tags (iteration + 1)
-    SolveCtx solve;
-    long long* stamps;   // MCC_DIAG builds: [8 * grid]
-    PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
-    double* prev2;       // m > 30 warm solve: [2][prev_stride] copy of [S | r] for the helper (null: off)
-    int prev_stride;
-};
+
 
 // The m > 30 solve with the previous step's inverse (the "warm" solve, solve_large in
 // mcc_kernels.hip): a resident helper kernel on a side stream (k_sinv_helper) inverts each update

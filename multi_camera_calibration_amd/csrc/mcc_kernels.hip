@@ -781,11 +781,15 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 // two doubles (16-B aligned) in one 16-B write-through store: MI355X_MICROARCH.md prices 8-B
 // `sc1` stores at 2.7x the per-byte time of 16-B ones (one fabric write per lane each)
 typedef double f64x2_t __attribute__((ext_vector_type(2)));
+// The s_nop covers the VMEM store-data hazard the compiler does not see through inline asm: a store of
+// more than 64 bits whose data VGPRs the next VALU instruction overwrites needs a wait state (k_group's
+// slot stores, round 5: the compiler reused the first store's data registers for the next address at
+// once, and the slots held addresses)
 __device__ __forceinline__ void st_sc1_x2(double* p, double a, double b) {
     f64x2_t v;
     v.x = a;
     v.y = b;
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ double ld_sc1(const double* p) {
     return __longlong_as_double((long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -2958,7 +2962,7 @@ __device__ __forceinline__ void st_sys_x2(double* p, double a, double b) {
     f64x2_t v;
     v.x = a;
     v.y = b;
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");   // (st_sc1_x2's hazard)
 }
 __device__ __forceinline__ unsigned ld_sys_u32(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3232,7 +3236,7 @@ __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* er
 __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool ack) {
     State* st = a.state;
     const int tid = threadIdx.x, nt = blockDim.x, m = a.global_dim, W = 2 * m;
-    if (ack && a.spare_delay > 0) {   // test (MCC_SPARE_DELAY_US): a spare scheduled late
+    if ((ack || a.fold) && a.spare_delay > 0) {   // test (MCC_SPARE_DELAY_US): a spare scheduled late
         if (tid == 0) {
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < a.spare_delay) __builtin_amdgcn_s_sleep(8);
@@ -3245,12 +3249,18 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool 
     const int done = st->done, it = st->iter, pend = st->pending;
     if (done) return;   // (the photos see the same word)
     const unsigned seq = (unsigned)it;
-    double* out = a.ssinv + (size_t)(it & 1) * m * m;
+    // k_group's folded step (a.fold): the final workgroup of THIS launch reads the inverse -- sc1
+    // stores into fiv, each word its own flag, and the status word +(it + 1) (an inverse) or -(it + 1)
+    // (none) as a double, written after this workgroup read the packed system and the state: the final workgroup
+    // writes neither before it has seen the status
+    const bool fold = a.fold != 0;
+    double* out = fold ? a.fiv : a.ssinv + (size_t)(it & 1) * m * m;
     int* okp = a.ssinv_ok + (it & 1);
     __shared__ int ok_s;
     if (!pend) {   // no update step before this one: no system to precondition with
         if (tid == 0) {
-            *okp = 0;
+            if (fold) st_sc1(a.fiv + m * m, -(double)(it + 1));   // (a double: -1 as bits would read as empty)
+            else *okp = 0;
             if (ack) __hip_atomic_store(&st->spare_ack, seq + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
@@ -3292,9 +3302,14 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool 
     if (ok)
         for (int t = tid; t < m * m; t += nt) {
             const int i = t / m, j = t % m;
-            out[t] = A[i * W + m + j] / A[i * W + i];
+            const double v = A[i * W + m + j] / A[i * W + i];
+            if (fold) st_sc1(out + t, v);
+            else out[t] = v;
         }
-    if (tid == 0) *okp = ok ? it + 1 : 0;
+    if (tid == 0) {
+        if (fold) st_sc1(a.fiv + m * m, ok ? (double)(it + 1) : -(double)(it + 1));
+        else *okp = ok ? it + 1 : 0;
+    }
 }
 
 // x = S^-1 r by refinement with Iv (m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
@@ -3536,17 +3551,15 @@ constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <
 // independent unconditional loads: a load under a per-item condition, or a loop whose stores wait
 // on its loads, costs a round trip per load or iteration: 5 us at config4 in the first form), and
 // the sums are formed from LDS.
+__device__ __forceinline__ void schur_finish(const SchurArgs& a, int nparts, int iter, double cn0, double cn1,
+                                             int err_now, bool iv, long long* srow);
 __device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) {
     State* st = a.state;
     const int tid = threadIdx.x;
     if (!arrive_last_sc1(a.counter, (int)gridDim.x)) return;
     STAMPP(a.stamps, kSchurStampStride, 2);
-    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    const int m = a.m;
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    double* S = sm;          // m*m
-    double* r = sm + m * m;  // m
-    __shared__ double norms[2];
-    const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
     // the previous system's inverse from k_group's spare workgroup
     double* Iv = a.ssinv && a.fuse_solve ? sm + m * m + m : nullptr;
     double* itm = sm + schur_items_offset(m, a.fuse_solve, a.ssinv != nullptr);   // [grid][48]
@@ -3593,27 +3606,63 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) 
     if (tid == 0) iv_ok = ivok;
     __syncthreads();
     STAMPP(a.stamps, kSchurStampStride, 8);   // the batch landed in LDS
+    schur_finish(a, (int)gridDim.x, iter, cn0, cn1, err_now, Iv && iv_ok,
+                 a.stamps ? a.stamps + kSchurStampStride * (size_t)blockIdx.x : nullptr);
+}
+// The final sums of the one-level hand-off and the solve, from LDS: every partial (48 per item or norm
+// chunk, nparts of them) in itm, the block ranges in sbi, the inverse (iv) after S and r -- k_schur's
+// last arriver (schur_one_level) and k_group's folded final workgroup (fold_final) both land them there
+// srow: this workgroup's MCC_DIAG stamp row (k_schur's by grid index, the folded final's after the items)
+__device__ __forceinline__ void schur_finish(const SchurArgs& a, int nparts, int iter, double cn0, double cn1,
+                                             int err_now, bool iv, long long* srow) {
+    State* st = a.state;
+    const int tid = threadIdx.x;
+    const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    double* S = sm;          // m*m
+    double* r = sm + m * m;  // m
+    __shared__ double norms[2];
+    const bool lds = a.fuse_solve && a.peer.nranks == 0;   // single GPU: solve from the sums directly
+    double* Iv = iv ? sm + m * m + m : nullptr;
+    const double* itm = sm + schur_items_offset(m, a.fuse_solve, a.ssinv != nullptr);   // [nparts][48]
+    const int* sbi = reinterpret_cast<const int*>(itm + 48 * (size_t)nparts);          // [nblk + 1]
     // the sums first, every global store after them: a loop entered with a store in flight gets
     // an s_waitcnt vmcnt(0) at its head (the compiler's pre-loop flush), which waits for the store's
     // completion -- 1.5 us at config4 when the packed stores sat between the sums' loops
     constexpr int EU = (15 * 48 + kSchurThreads - 1) / kSchurThreads;   // entries per thread (m <= 30)
     const int nent = a.nblk * 48;
     double ev[EU];
+    const bool sl = tid < kSchurThreads;   // (the folded final workgroup has k_group's 256 or 512 threads)
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
         const int t = tid + u * kSchurThreads;
         double v = 0.0;
-        if (t < nent) {
+        if (sl && t < nent) {
             const int blk = t / 48, e = t % 48;
             const int k0 = sbi[blk], nk = sbi[blk + 1] - k0;
-            for (int q = 0; q < nk; ++q) v += itm[48 * (k0 + q) + e];   // item order (level 1's sums)
+            // item order (level 1's sums); the first 8 items' words read in one go (a loop with a
+            // runtime bound waited for each LDS read in turn: ~1.8 us from the batch to the placed sums)
+            double w[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = itm[48 * (k0 + (q < nk ? q : 0)) + e];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < nk) v += w[q];
+            for (int q = 8; q < nk; ++q) v += itm[48 * (k0 + q) + e];
         }
         ev[u] = v;
     }
     double nrm = 0.0;
     if (tid < 2) {
         const int w = tid;   // 0: normG2, 1: normX2 of the last update
-        for (int k = a.n_items; k < (int)gridDim.x; ++k) nrm += itm[48 * k + w];   // chunk order
+        const int nc = nparts - a.n_items;
+        double cw[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cw[q] = itm[48 * (a.n_items + (q < nc ? q : 0)) + w];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (q < nc) nrm += cw[q];   // chunk order
+        for (int k = a.n_items + 8; k < nparts; ++k) nrm += itm[48 * k + w];
         if (a.rank == 0) nrm += w ? cn1 : cn0;
         if (iter <= 0) nrm = 0.0;
         nrm = photo_flag_norm(err_now, w, nrm);
@@ -3622,7 +3671,7 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) 
 #pragma unroll
     for (int u = 0; u < EU; ++u) {
         const int t = tid + u * kSchurThreads;
-        if (t >= nent) continue;
+        if (!sl || t >= nent) continue;
         const int blk = t / 48, e = t % 48;
         int b1 = 0;   // the block's row: the last b with first_block(b) <= blk (nb <= 5)
 #pragma unroll
@@ -3647,7 +3696,7 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) 
         }
     }
     if (tid < 2) a.packed[ntri + 2 * m + tid] = nrm;
-    STAMPP(a.stamps, kSchurStampStride, 9);   // sums placed (thread 0)
+    SSTAMP(srow, 9, 0);   // sums placed (thread 0)
     if (!a.fuse_solve) return;
     __syncthreads();   // the packed system and the norms (this workgroup's global stores and LDS)
     if (a.peer.nranks > 0) {
@@ -3667,11 +3716,11 @@ __device__ __forceinline__ void schur_one_level(const SchurArgs& a, int iter_e) 
         if (tid < 2) norms[tid] = a.packed[ntri + 2 * m + tid];
         __syncthreads();
     }
-    STAMPP(a.stamps, kSchurStampStride, 3);
+    SSTAMP(srow, 3, 0);
     SolveCtx sc = a.solve;
-    sc.stamps = a.stamps ? a.stamps + kSchurStampStride * (size_t)blockIdx.x : nullptr;   // slots 4..6 of this row
-    solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, Iv && iv_ok ? Iv : nullptr);
-    STAMPP(a.stamps, kSchurStampStride, 7);
+    sc.stamps = srow;   // slots 4..6 of this row
+    solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, Iv);
+    SSTAMP(srow, 7, 0);
 }
 #ifndef MCC_SCHUR_LOADS
 #define MCC_SCHUR_LOADS 32
@@ -4183,7 +4232,9 @@ hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int m
 template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
     // + the spare workgroup of the m <= 30 warm solve (small_inverse)
-    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), dim3(a.n_pgroups + (a.ssinv ? 1 : 0)),
+    // (+ the folded reduction's item, norm-chunk and final workgroups)
+    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>),
+                       dim3(a.n_pgroups + (a.ssinv ? 1 : 0) + (a.fold ? a.fold_parts + 1 : 0)),
                        dim3(kGroupRound * L), shmem, s, a);
     return hipGetLastError();
 }

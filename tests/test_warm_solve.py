@@ -278,3 +278,39 @@ def test_timing_probe_keeps_the_trajectory(cfg, views, env):
         finally:
             ba.close()
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("views", [200, 1000])
+def test_folded_group_step_is_bitwise_the_two_kernel_step(views):
+    """k_group's step with k_schur's reduction and the solve folded into the same launch (the default
+    while the items fit: LinArgs::fold, DESIGN.md section 3) against k_group -> k_schur (MCC_GFOLD=0):
+    the same sums in the same order, so the optimize and the free-running steps are bitwise equal.  The
+    folded consumers poll the hand-off words themselves (kFoldEmpty until written): with the spare
+    workgroup held back 300 us (its status word is what the final workgroup waits for before it writes
+    the packed system and the state) the bits do not move.  1 000 views is config4 itself (250 groups on
+    256 CUs: the items start only when groups exit).  src/multicalib.cpp:462-514."""
+    p = rig.make_config("config4", n_views=views)
+    runs = []
+    for env in ({"MCC_GFOLD": "0"}, {}, {"MCC_SPARE_DELAY_US": "300"}):
+        ba = make(p, dict(env, MCC_FUSED="0", MCC_SOLVE_STATS="1"))
+        try:
+            assert ba.step_kernels() == "k_group"
+            try:
+                x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+            except api.MccError as e:
+                raise AssertionError(f"{env}: {e}")
+            ba.set_params(p.x0)
+            ba.step(24)
+            ba.check()
+            xs = ba.get_params()
+            st = ba.solve_stats()
+        finally:
+            ba.close()
+        runs.append((x, it, xs, st))
+    (x0, it0, xs0, st0) = runs[0]
+    for (x, it, xs, st) in runs[1:]:
+        assert it == it0
+        assert np.array_equal(x, x0) and np.array_equal(xs, xs0)
+        for k in ("warm", "corrections", "fallbacks", "direct"):
+            assert st[k] == st0[k], (st0, st)
+    assert st0["warm"] > 0

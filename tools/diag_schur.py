@@ -62,6 +62,6 @@ for rep in range(3):
               f"items summed max {q(items[:, 1].max() - t0)}, level-1 max {q(lv1.max() - t0) if len(lv1) else '-'}")
     for f in fin:
         names = ["solve entry", "GJ start (w1)", "GJ end (w1)", "final: before packed loads", "stop-test barrier", "-",
-                 "camera update", "end", "one level: batch landed", "sums placed"]
+                 "camera update", "end", "one level: batch landed", "sums placed", "fold: final start"]
         print("  final WG: " + ", ".join(f"{n} {q(v - t0)}" for n, v in zip(names, f) if v))
 ba.close()
