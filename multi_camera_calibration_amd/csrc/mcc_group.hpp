@@ -331,9 +331,11 @@ __device__ __forceinline__ void fold_item(const LinArgs& la, int item) {
         int next = 0;
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
         for (;;) {
+            // the slots not summed yet (the summed ones re-read at the first slot's address instead)
             double v[kFoldSlots];
 #pragma unroll
-            for (int u = 0; u < kFoldSlots; ++u) v[u] = ld_sc1(pp + (size_t)sz * (sub + kSub * min(u, ns - 1)));
+            for (int u = 0; u < kFoldSlots; ++u)
+                v[u] = ld_sc1(pp + (size_t)sz * (sub + kSub * (u < next ? 0 : min(u, ns - 1))));
 #pragma unroll
             for (int u = 0; u < kFoldSlots; ++u)
                 if (u == next && u < ns && fold_valid(v[u])) {
@@ -342,10 +344,8 @@ __device__ __forceinline__ void fold_item(const LinArgs& la, int item) {
                 }
             if (next >= ns) break;
             if (fold_timed_out(la, t0)) { fail = 1; break; }
-            __builtin_amdgcn_s_sleep(1);
         }
         s += 0.0;   // (k_schur adds its batch's zero padding: -0.0 becomes +0.0 there too)
-        for (int u = 0; u < ns; ++u) fold_empty(const_cast<double*>(pp) + (size_t)sz * (sub + kSub * u));
     }
     if (sub < kSub) part[sub][q] = s;
     __syncthreads();
@@ -355,6 +355,11 @@ __device__ __forceinline__ void fold_item(const LinArgs& la, int item) {
         st_sc1(a.item_out + 48 * (size_t)item + tid, t);
     }
     SSTAMP(srow, 1, 0);
+    // the slots back to kFoldEmpty, after the partial (ahead of it these stores held its store up)
+    if (ns > 0 && q < sz) {
+        double* pp = const_cast<double*>(a.pairprod) + (size_t)it.y + q;
+        for (int u = 0; u < ns; ++u) fold_empty(pp + (size_t)sz * (sub + kSub * u));
+    }
 }
 
 // norm-chunk workgroup c: 256 photos' ||G||^2, ||x||^2 (k_schur's norm chunk: a fixed butterfly per
@@ -382,8 +387,6 @@ __device__ __forceinline__ void fold_chunk(const LinArgs& la, int c) {
                 if (fold_timed_out(la, t0)) { fail = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
-            double* fw = la.fnorm + 4 * (size_t)p;
-            fold_empty(fw); fold_empty(fw + 1); fold_empty(fw + 2);
         }
         g = wave_sum(g);
         x = wave_sum(x);
@@ -402,6 +405,11 @@ __device__ __forceinline__ void fold_chunk(const LinArgs& la, int c) {
         st_sc1(a.item_out + 48 * (size_t)(a.n_items + c) + tid, v);
     }
     SSTAMP(srow, 1, 0);
+    const int p = c * kSchurThreads + tid;
+    if (tid < kSchurThreads && p < a.n_photos) {   // back to kFoldEmpty, after the partial
+        double* fw = la.fnorm + 4 * (size_t)p;
+        fold_empty(fw); fold_empty(fw + 1); fold_empty(fw + 2);
+    }
 }
 
 // the final workgroup: every partial (48 per item / chunk) and the spare's inverse with its status into
@@ -493,6 +501,12 @@ __device__ __forceinline__ void fold_final_u(const LinArgs& la) {
 // partials: the copy, a barrier and the runtime-bounded LDS sums (~1.8 us from the landed batch to the
 // placed sums at config4) leave the tail.
 constexpr int kFoldKI = 8;   // words per thread
+__device__ __forceinline__ void fold_final_reset(const LinArgs& la, const double* const* src, unsigned have, bool useiv) {
+#pragma unroll
+    for (int q = 0; q < kFoldKI; ++q)
+        if ((have >> q) & 1) fold_empty(const_cast<double*>(src[q]));
+    if (threadIdx.x == 0 && useiv) fold_empty(la.fiv + la.fsa.m * la.fsa.m);
+}
 __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
     const SchurArgs& a = la.fsa;
     State* st = a.state;
@@ -554,11 +568,14 @@ __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
     double kv[kFoldKI];
     unsigned have = 0;
     double stt = -1.0;
+    // each thread polls its own words until they have all landed (one memory round trip per pass, no
+    // barrier per pass), then one barrier; words already in registers are re-read at the status word's
+    // address (one request per wave) instead of their own
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     for (;;) {
         double v[kFoldKI];
 #pragma unroll
-        for (int q = 0; q < kFoldKI; ++q) v[q] = ld_sc1(src[q]);
+        for (int q = 0; q < kFoldKI; ++q) v[q] = ld_sc1(((have >> q) & 1) ? la.fiv + m * m : src[q]);
         if (useiv) stt = ld_sc1(la.fiv + m * m);
         int pend = tid == 0 && useiv && !fold_valid(stt) ? 1 : 0;
 #pragma unroll
@@ -571,22 +588,25 @@ __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
                 ++pend;   // the inverse's words are due unless the status says "none"
             }
         }
-        if (!__syncthreads_or(pend)) break;
-        if (tid == 0 && (long long)__builtin_amdgcn_s_memrealtime() - t0 >= la.spare_wait) {
+        if (!pend) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 >= la.spare_wait) {
+            s_fail = 1;
+            break;
+        }
+    }
+    __shared__ double s_stt;
+    if (tid == 0) s_stt = stt;   // (thread 0 waited for the status; a thread whose own words landed
+                                 // first may have read it empty)
+    __syncthreads();
+    if (s_fail) {
+        if (tid == 0) {
             atomicOr(&st->error, kErrWarmTimeout);
             st->done = 1;
-            s_fail = 1;
         }
-        __syncthreads();
-        if (s_fail) return;
+        return;
     }
     SSTAMP(srow, 8, 0);   // every word landed
-    const bool ivok = useiv && stt > 0.0;
-    // every word back to kFoldEmpty for the next launch's producers
-#pragma unroll
-    for (int q = 0; q < kFoldKI; ++q)
-        if ((have >> q) & 1) fold_empty(const_cast<double*>(src[q]));
-    if (tid == 0 && useiv) fold_empty(la.fiv + m * m);
+    const bool ivok = useiv && s_stt > 0.0;
     if (kind == 1 && cnt > 0) {
         double v = 0.0;
 #pragma unroll
@@ -631,10 +651,16 @@ __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
             if (q < cnt) Iv[j0 + q * nivt] = kv[q];
     }
     SSTAMP(srow, 9, 0);   // sums placed (thread 0)
-    if (!a.fuse_solve) return;
+    if (!a.fuse_solve) {
+        fold_final_reset(la, src, have, useiv);
+        return;
+    }
     __syncthreads();   // S, r, the inverse and the norms in LDS
     if (a.peer.nranks > 0) {
-        if (!peer_exchange(a.peer, st, a.packed)) return;
+        if (!peer_exchange(a.peer, st, a.packed)) {
+            fold_final_reset(la, src, have, useiv);
+            return;
+        }
         for (int t = tid; t < ntri + m; t += nt) {
             const double v = a.packed[t];
             if (t < ntri) {
@@ -654,6 +680,9 @@ __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
     sc.stamps = srow;
     solve_global<false>(sc, S, r, norms[0], norms[1], nullptr, ivok ? Iv : nullptr);
     SSTAMP(srow, 7, 0);
+    // every word back to kFoldEmpty for the next launch's producers (after the solve: ahead of it these
+    // 4 000 write-through stores held up the placement's)
+    fold_final_reset(la, src, have, useiv);
 }
 // (one batch width per k_group shape: the host keeps 48 parts + m^2 + 1 within k_schur's one-level
 // bound, kSchurOneLevelLoads x 256 words)
