@@ -457,6 +457,14 @@ def main():
                             "flops_per_corner": fp["fp64_flops_per_corner"],
                             "source": "profiles/fp64_*.json (rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes, "
                                       "an upper bound) / the event-timed launch"}
+        sq = load_profile("sq", args.config, views_per_rank)
+        ks = [k for k in (sq or {}).get("kernels", {}) if k in kern and "valu_issue_frac" in sq["kernels"][k]]
+        if ks:
+            # the counter-based frac counts every lane of every FP64 instruction; the SIMDs' VALU issue
+            # share (SQ pass) is the utilisation figure
+            out["fp64_valu"]["valu_issue_frac"] = {k: round(sq["kernels"][k]["valu_issue_frac"], 4) for k in ks}
+            out["fp64_valu"]["valu_issue_source"] = ("profiles/sq_*.json: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES "
+                                                     "x waves per SIMD (tools/pmc_sq.sh)")
     if solve["warm"] or solve["direct"]:
         out["warm_solve"] = solve
     if strong:

@@ -73,7 +73,7 @@ def build(force: bool = False) -> str:
     stale = any(not os.path.exists(o) for o in outs) or any(
         os.path.getmtime(s) > min(os.path.getmtime(o) for o in outs) for s in srcs)
     if force or stale:
-        subprocess.run(["make", "-s", "--no-print-directory", "-C", _HERE, "-j4", "all"], check=True)
+        subprocess.run(["make", "-s", "--no-print-directory", "-C", _HERE, "-j8", "all"], check=True)
     if os.path.exists(REF_SAMPLE_SRC):
         # optional: the reference's sample compiled against the compatibility headers (the test
         # that needs it, tests/test_reference_sample.py, builds it itself and reports a failure);

@@ -31,6 +31,23 @@
 #include "mcc_device.hpp"
 #include "mcc_internal.h"
 
+// The library is built from this file compiled once per part (-DMCC_PART=0..5, in parallel: one
+// translation unit took ~5 minutes).  Each part holds the non-template kernels and the launch
+// wrappers (and so the template instantiations) of one family; without MCC_PART it is all of them.
+//   0 host helpers, peers, backsub, project_error   1 k_linearize   2 k_group L = 16
+//   3 k_group L = 32   4 the split step's k_prep / k_prep4 / k_edge / k_photo   5 k_schur, k_solve
+#ifdef MCC_PART
+#define MCC_IN(n) (MCC_PART == (n))
+#else
+#define MCC_IN(n) 1
+#endif
+// per-part kernel attributes (mcc_set_kernel_attrs, part 0, calls them)
+hipError_t mcc_attrs_linearize(size_t shmem);
+hipError_t mcc_attrs_group16(size_t shmem);
+hipError_t mcc_attrs_group32(size_t shmem);
+hipError_t mcc_attrs_photo(size_t shmem);
+hipError_t mcc_attrs_solve(size_t shmem);
+
 namespace mcc {
 
 // ---------------------------------------------------------------- diagnostic stamps
@@ -2144,6 +2161,7 @@ __global__ __launch_bounds__(64, (MODEL == MCC_MODEL_OMNI || RATIONAL || PRISM) 
 #ifndef MCC_PHOTO_RPT
 #define MCC_PHOTO_RPT 1   // rows of a camera-pair block per k_photo pair task (2, 3: fewer waves, slower)
 #endif
+#if MCC_IN(4)
 #ifdef MCC_PHOTO_OCC
 __global__ __launch_bounds__(256, MCC_PHOTO_OCC) void k_photo(LinArgs a) {
 #else
@@ -2417,6 +2435,7 @@ __global__ __launch_bounds__(256) void k_photo(LinArgs a) {
 #endif
     SSTAMP(stp, 5, 0);
 }
+#endif  // MCC_IN(4)
 
 // ---------------------------------------------------------------- global solve (one workgroup)
 // Stop test (src/multicalib.cpp:475-477), elimination of the reduced camera system (m <= 128),
@@ -3134,6 +3153,7 @@ __device__ bool gj_inverse_blocked(double* A, double* PV, int M) {
 // n_systems systems, when a k_solve reports that no more systems follow (sync[2]: the loop
 // stopped, a failed step, a peer timeout), or after kHelperIdleTicks without a new system: every
 // wave reaches the exit.
+#if MCC_IN(5)
 __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m, int n_systems) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ unsigned ep_s;
@@ -3203,6 +3223,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         seen = e;
     }
 }
+#endif  // MCC_IN(5)
 
 __device__ void gj_dispatch(const double* S, double* r, int m, int lane, int* err, int* bad_lds = nullptr) {
     switch (m) {
@@ -3314,59 +3335,72 @@ __device__ __forceinline__ void small_inverse(const LinArgs& a, double* A, bool 
 
 // x = S^-1 r by refinement with Iv (m x m) on one wave: x0 = Iv r, x += Iv (r - S x) until every
 // equation holds to its own scale, |r - S x|_i <= 64 eps (|S| |x| + |r|)_i (the warm solve's test),
-// at most kWarmMaxIters corrections, each cutting the error fourfold.  Lane i holds row i of S and of
-// Iv in registers (read once from LDS); the vectors reach every lane by v_readlane with compile-time
-// lanes (the register Gauss-Jordan's broadcast), so a correction is 2m broadcasts and 3m FMAs with
-// no LDS round trip -- round 4's first form read S, Iv and the vectors from LDS per product and took
-// ~3 us at m = 18, longer than the elimination.  On success r holds x.
+// at most kWarmMaxIters corrections, each cutting the error fourfold.  Two lanes share row i (lanes
+// 2i, 2i+1, m <= 30): each holds half of the row of S and of Iv in registers (read once) and takes
+// the matching half of the vector from a 32-entry LDS slot that the even lanes write, so a product
+// is m/2 LDS reads and FMAs per lane plus one DPP exchange of the two half sums.  Round 4 broadcast
+// the vector by m v_readlane pairs per product (~1.9 us of refinement at m = 18); round 4's first
+// form read S and Iv from LDS per product (~3 us).  On success r holds x.
 template <int MM>
-__device__ __forceinline__ bool small_refine_reg(const double* S, double* r, const double* Iv, int m, int lane, int* corr) {
-    const int li = lane < m ? lane : 0;
+__device__ __forceinline__ bool small_refine_reg(const double* S, double* r, const double* Iv, int m, int lane, int* corr,
+                                                 double* vb) {
+    constexpr int H = MM / 2;
     // a necessary condition for S > 0 that the direct elimination's pivots would test: a non-positive
     // (or NaN) diagonal entry sends the system to gj_rows, which reports it (MCC_ENOTPD)
+    const int li = lane < m ? lane : 0;
     if (__builtin_amdgcn_ballot_w64(lane < m && !(S[li * m + li] > 0.0))) return false;
-    double sr[MM], ir[MM];
+    const int i = lane >> 1, c0 = (lane & 1) * H;
+    const bool act = i < MM, wr = act && (lane & 1) == 0;
+    const int ri = act ? i : 0;
+    double sr[H], ir[H], w[H];
 #pragma unroll
-    for (int j = 0; j < MM; ++j) {
-        sr[j] = S[li * m + (j < m ? j : 0)];
-        ir[j] = Iv[li * m + (j < m ? j : 0)];
+    for (int k = 0; k < H; ++k) {
+        sr[k] = S[ri * MM + c0 + k];
+        ir[k] = Iv[ri * MM + c0 + k];
+        w[k] = r[c0 + k];
     }
-    const double rr = lane < m ? r[li] : 0.0;
-    double x = 0.0;
+    const double rr = r[ri];
+    double p = 0.0;
 #pragma unroll
-    for (int j = 0; j < MM; ++j)
-        if (j < m) x = fma(ir[j], readlane_f64(rr, j), x);
+    for (int k = 0; k < H; ++k) p = fma(ir[k], w[k], p);
+    double x = p + dpp_f64<kDppXor1>(p);   // both lanes of the row: the same sum, the same rounding
     constexpr double kTol = 64.0 * 1.1102230246251565e-16;
     bool conv = false;
     double qprev = 0.0;
     for (int it = 0;; ++it) {
-        double res = rr, sa = fabs(rr);
+        if (wr) vb[i] = x;
+        wave_sync_lds();
+        double ps = 0.0, pa = 0.0;
 #pragma unroll
-        for (int j = 0; j < MM; ++j) {
-            if (j < m) {
-                const double xj = readlane_f64(x, j);
-                res = fma(-sr[j], xj, res);
-                sa = fma(fabs(sr[j]), fabs(xj), sa);
-            }
+        for (int k = 0; k < H; ++k) {
+            const double xj = vb[c0 + k];
+            ps = fma(sr[k], xj, ps);
+            pa = fma(fabs(sr[k]), fabs(xj), pa);
         }
-        const double q = lane < m ? (fabs(res) / fmax(sa, 1e-300)) : 0.0;
+        wave_sync_lds();
+        const double res = rr - (ps + dpp_f64<kDppXor1>(ps));
+        const double sa = fabs(rr) + (pa + dpp_f64<kDppXor1>(pa));
+        const double q = act ? (fabs(res) / fmax(sa, 1e-300)) : 0.0;
         const double qm = wave_max(q == q ? q : 1.0);
         conv = qm <= kTol;
         if (conv || it >= kWarmMaxIters || (it > 0 && !(qm <= 0.25 * qprev))) break;
         qprev = qm;
         *corr = it + 1;
-        double dx = 0.0;
+        if (wr) vb[i] = res;
+        wave_sync_lds();
+        double pd = 0.0;
 #pragma unroll
-        for (int j = 0; j < MM; ++j)
-            if (j < m) dx = fma(ir[j], readlane_f64(res, j), dx);
-        x += dx;
+        for (int k = 0; k < H; ++k) pd = fma(ir[k], vb[c0 + k], pd);
+        wave_sync_lds();
+        x += pd + dpp_f64<kDppXor1>(pd);
     }
-    if (conv && lane < m) r[lane] = x;   // rr was read by every lane above (one wave: in order)
+    if (conv && wr) r[i] = x;   // r was read by every lane above (one wave: in order)
     return conv;
 }
-__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, int m, int lane, int* corr) {
+__device__ __forceinline__ bool small_refine(const double* S, double* r, const double* Iv, int m, int lane, int* corr,
+                                             double* vb) {
     switch (m) {
-#define SR(M) case M: return small_refine_reg<M>(S, r, Iv, m, lane, corr);
+#define SR(M) case M: return small_refine_reg<M>(S, r, Iv, m, lane, corr, vb);
         SR(6) SR(12) SR(18) SR(24) SR(30)
 #undef SR
         default: return false;
@@ -3387,6 +3421,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     SSTAMP(a.stamps, 0, 0);
     const bool wrm = LARGE && warm_on(warm, m);
     __shared__ int s_sm_ok, s_sm_corr;   // m <= 30: the refinement converged, with this many corrections
+    __shared__ double s_rv[32];          // m <= 30: the refinement's vector exchange
     WarmStage ws;
     if (wrm) warm_issue(S, m, ws);
     if (wrm && tid == 64) warm_check(*warm, &s_use, &s_ep);
@@ -3425,7 +3460,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
         // with the previous system's inverse (k_schur, m <= 30): refinement, else / on failure the
         // register Gauss-Jordan
         int corr = 0;
-        const bool ok = Iv && small_refine(S, r, Iv, m, tid - 64, &corr);
+        const bool ok = Iv && small_refine(S, r, Iv, m, tid - 64, &corr, s_rv);
         if (tid == 64) {   // (statistics, read after the barriers below)
             s_sm_ok = ok;
             s_sm_corr = corr;
@@ -3725,6 +3760,7 @@ __device__ __forceinline__ void schur_finish(const SchurArgs& a, int nparts, int
 #ifndef MCC_SCHUR_LOADS
 #define MCC_SCHUR_LOADS 32
 #endif
+#if MCC_IN(5)
 __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     State* st = a.state;
     if (st->done) return;
@@ -3867,8 +3903,10 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     solve_global<false>(sc, S, r, norms[0], norms[1]);
     STAMPP(a.stamps, kSchurStampStride, 7);
 }
+#endif  // MCC_IN(5)
 
 // ---------------------------------------------------------------- k_solve (multi-GPU: after the all-reduce)
+#if MCC_IN(5)
 __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveArgs a) {
     if (a.ctx.state->done) {
         warm_stop(a.warm);
@@ -3898,21 +3936,25 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(SolveArgs a) {
     __syncthreads();
     solve_global<false>(a.ctx, S, r, a.packed[ntri + 2 * m], a.packed[ntri + 2 * m + 1]);
 }
+#endif  // MCC_IN(5)
 
 // This rank's packed system -> every peer's inbox from many workgroups (the m > 30 split step, in
 // front of k_solve, which then only receives): 2 Lc LL words per peer -- 68 KB at m = 90, ~480 KB
 // per rank at 8 ranks -- are too many 8-B system-scope stores for one workgroup's store issue.
 // The epoch is read here and advanced only by k_solve's exchange after this kernel has ended.
+#if MCC_IN(0)
 __global__ __launch_bounds__(256) void k_peer_push(PeerCtx pc, const State* st, const double* vals) {
     if (st->done) return;
     const unsigned ep = st->epoch + 1u;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < pc.Lc; t += gridDim.x * blockDim.x)
         peer_send(pc, ep, t, vals[t]);
 }
+#endif  // MCC_IN(0)
 
 // ---------------------------------------------------------------- mcc_debug_solve
 // The m > 30 dense solve alone (k_solve's elimination on a packed SPD system [S upper | r]):
 // x = S^-1 r, the error bits, and per-phase stamps.  Test and measurement only.
+#if MCC_IN(5)
 __global__ __launch_bounds__(1024) void k_debug_solve(const double* packed, double* xout, int m, int* err,
                                                        long long* gst) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -3922,6 +3964,7 @@ __global__ __launch_bounds__(1024) void k_debug_solve(const double* packed, doub
     GJB_STAMP(63);
     for (int t = threadIdx.x; t < m; t += blockDim.x) xout[t] = sm[t];
 }
+#endif  // MCC_IN(5)
 
 // ---------------------------------------------------------------- peer transport: handshake, max
 // k_peer_handshake: round 1 sends a (rank, index) pattern over the whole inbox width and checks
@@ -3931,6 +3974,7 @@ __global__ __launch_bounds__(1024) void k_debug_solve(const double* packed, doub
 __device__ __forceinline__ double peer_pattern(int rank, int t) {
     return (double)(rank + 1) * 1.0e6 + (double)t * 0.123456789 + 1.0 / 3.0;
 }
+#if MCC_IN(0)
 __global__ __launch_bounds__(256) void k_peer_handshake(PeerCtx pc, State* st, double* out) {
     __shared__ unsigned ep_s;
     __shared__ int bad_s, to_s;
@@ -3972,9 +4016,11 @@ __global__ __launch_bounds__(256) void k_peer_handshake(PeerCtx pc, State* st, d
         st->epoch = ep2;
     }
 }
+#endif  // MCC_IN(0)
 
 // k_peer_max: v[0] <- max over ranks (the bench's max-over-ranks timing and the barrier when no
 // RCCL communicator exists, e.g. several ranks on one device).  One thread.
+#if MCC_IN(0)
 __global__ void k_peer_max(PeerCtx pc, State* st, double* v) {
     if (threadIdx.x != 0) return;
     const unsigned ep = st->epoch + 1u;
@@ -3988,10 +4034,12 @@ __global__ void k_peer_max(PeerCtx pc, State* st, double* v) {
     st->epoch = ep;
     if (to) st->error |= 4;
 }
+#endif  // MCC_IN(0)
 
 // ---------------------------------------------------------------- k_backsub
 // one thread per photo: dp = L^-T (z - sum_e Y_e^T dg_e); with do_update the float32 update
 // (flush of a pending update), otherwise only deltaX.
+#if MCC_IN(0)
 __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.n_photos) return;
@@ -4017,6 +4065,7 @@ __global__ __launch_bounds__(256) void k_backsub(BacksubArgs a) {
         a.photo_norm[2 * p + 1] = x2;
     }
 }
+#endif  // MCC_IN(0)
 
 // ---------------------------------------------------------------- k_project_error
 // computeProjectError (src/mymulticalib.cpp:820-939, src/multicalib.cpp:895-1006,
@@ -4147,6 +4196,7 @@ __global__ __launch_bounds__(64) void k_project_error(ErrArgs a) {
 // ---------------------------------------------------------------- launch wrappers
 using namespace mcc;
 
+#if MCC_IN(1)
 template <int MODEL>
 static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem, hipStream_t s, bool rational, int prism) {
     const dim3 grid(n_photos + (a.ssinv ? 1 : 0));   // + the m <= 30 warm solve's spare workgroup
@@ -4157,7 +4207,27 @@ static hipError_t launch_lin_model(const LinArgs& a, int n_photos, size_t shmem,
     else hipLaunchKernelGGL((k_linearize<MODEL, false, false>), grid, dim3(256), shmem, s, a);
     return hipGetLastError();
 }
+hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, int prism, hipStream_t s) {
+    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.max_cpp);
+    switch (model) {
+        case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
+        case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
+        default: return launch_lin_model<MCC_MODEL_PINHOLE>(a, n_photos, shmem, s, rational, prism);
+    }
+}
+hipError_t mcc_attrs_linearize(size_t shmem) {
+    hipError_t err = hipSuccess;
+#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
+    for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
+                         SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true),
+                         SETA(2, true, true)})
+        if (e != hipSuccess) err = e;
+#undef SETA
+    return err;
+}
+#endif  // MCC_IN(1)
 
+#if MCC_IN(4)
 // split step: lanes per edge of k_edge (88-corner edges: 6 passes at 92% lane use, the 27-value
 // butterfly over 16 lanes is a quarter of a wave's)
 #ifndef MCC_EDGE_LANES
@@ -4203,6 +4273,12 @@ hipError_t mcc_launch_split(const LinArgs& a, int model, bool rational, int pris
     hipLaunchKernelGGL(k_photo, dim3(a.n_pgroups), dim3(256), photo_shmem, s, a);
     return hipGetLastError();
 }
+hipError_t mcc_attrs_photo(size_t shmem) {
+    return hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+}
+#endif  // MCC_IN(4)
+
+#if MCC_IN(0)
 
 size_t mcc_lin_shmem(int max_edges_per_photo, int n_cams, int m, int max_cpp) {
     const size_t lin = (size_t)max_edges_per_photo * sizeof(EdgeLds) + sizeof(PhotoLds) +
@@ -4220,15 +4296,9 @@ size_t mcc_solve_shmem(int m) {
     return std::max((size_t)(m * m + m), m > 30 ? std::max(blocked, warm) : 0) * sizeof(double);
 }
 
-hipError_t mcc_launch_linearize(const LinArgs& a, int model, int n_photos, int max_epp, bool rational, int prism, hipStream_t s) {
-    const size_t shmem = mcc_lin_shmem(max_epp, a.n_cams, a.global_dim, a.max_cpp);
-    switch (model) {
-        case MCC_MODEL_OMNI: return launch_lin_model<MCC_MODEL_OMNI>(a, n_photos, shmem, s, false, false);
-        case MCC_MODEL_DOUBLESIDE: return launch_lin_model<MCC_MODEL_DOUBLESIDE>(a, n_photos, shmem, s, rational, prism);
-        default: return launch_lin_model<MCC_MODEL_PINHOLE>(a, n_photos, shmem, s, rational, prism);
-    }
-}
+#endif  // MCC_IN(0)
 
+#if MCC_IN(2) || MCC_IN(3)
 template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
     // + the spare workgroup of the m <= 30 warm solve (small_inverse)
@@ -4261,12 +4331,6 @@ static hipError_t launch_group_l(const LinArgs& a, int model, bool rational, int
     if (prism) return launch_group_t<MCC_MODEL_PINHOLE, false, true, false, L>(a, shmem, s);
     return launch_group_t<MCC_MODEL_PINHOLE, false, false, false, L>(a, shmem, s);
 }
-hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, int prism, int lanes, size_t shmem,
-                            hipStream_t s) {
-    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
-    return lanes == 32 ? launch_group_l<32>(a, model, rational, prism, shmem, s)
-                       : launch_group_l<16>(a, model, rational, prism, shmem, s);
-}
 template <int L>
 static hipError_t set_group_attrs(size_t group_shmem) {
     hipError_t err = hipSuccess;
@@ -4281,6 +4345,25 @@ static hipError_t set_group_attrs(size_t group_shmem) {
 #undef SETG
     return err;
 }
+#endif  // MCC_IN(2) || MCC_IN(3)
+#if MCC_IN(3)
+hipError_t mcc_launch_group32(const LinArgs& a, int model, bool rational, int prism, size_t shmem, hipStream_t s) {
+    return launch_group_l<32>(a, model, rational, prism, shmem, s);
+}
+hipError_t mcc_attrs_group32(size_t shmem) { return set_group_attrs<32>(shmem); }
+#endif
+#if MCC_IN(2)
+hipError_t mcc_launch_group32(const LinArgs& a, int model, bool rational, int prism, size_t shmem, hipStream_t s);
+hipError_t mcc_launch_group(const LinArgs& a, int model, bool rational, int prism, int lanes, size_t shmem,
+                            hipStream_t s) {
+    if (a.n_photos <= 0 || a.n_edges <= 0) return hipSuccess;
+    return lanes == 32 ? mcc_launch_group32(a, model, rational, prism, shmem, s)
+                       : launch_group_l<16>(a, model, rational, prism, shmem, s);
+}
+hipError_t mcc_attrs_group16(size_t shmem) { return set_group_attrs<16>(shmem); }
+#endif
+
+#if MCC_IN(0)
 
 // The dynamic-LDS limits only ever grow within a process (per device): a graph captured for an
 // earlier, larger problem keeps launching with the LDS it was captured with after a smaller problem
@@ -4299,29 +4382,32 @@ hipError_t mcc_set_kernel_attrs(int max_epp, int n_cams, int m, int max_cpp, siz
     photo_shmem = hw[2] = std::max(hw[2], photo_shmem);
     ss = hw[3] = std::max(hw[3], ss);
     if (group_shmem > 64 * 1024) {
-        for (hipError_t e : {set_group_attrs<16>(group_shmem), set_group_attrs<32>(group_shmem)})
+        for (hipError_t e : {mcc_attrs_group16(group_shmem), mcc_attrs_group32(group_shmem)})
             if (e != hipSuccess) err = e;
     }
     if (shmem > 64 * 1024) {
-#define SETA(M, R, P) hipFuncSetAttribute((const void*)&k_linearize<M, R, P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem)
-        for (hipError_t e : {SETA(0, false, false), SETA(0, true, false), SETA(0, false, true), SETA(0, true, true),
-                             SETA(1, false, false), SETA(2, false, false), SETA(2, true, false), SETA(2, false, true),
-                             SETA(2, true, true)})
-            if (e != hipSuccess) err = e;
-#undef SETA
+        hipError_t e = mcc_attrs_linearize(shmem);
+        if (e != hipSuccess) err = e;
     }
     if (photo_shmem > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)&k_photo, hipFuncAttributeMaxDynamicSharedMemorySize, (int)photo_shmem);
+        hipError_t e = mcc_attrs_photo(photo_shmem);
         if (e != hipSuccess) err = e;
     }
     if (ss > 60 * 1024) {
-        hipError_t e1 = hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
-        hipError_t e2 = hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
-        hipError_t e3 = hipFuncSetAttribute((const void*)&k_sinv_helper, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss);
-        if (e1 != hipSuccess) err = e1;
-        if (e2 != hipSuccess) err = e2;
-        if (e3 != hipSuccess) err = e3;
+        hipError_t e = mcc_attrs_solve(ss);
+        if (e != hipSuccess) err = e;
     }
+    return err;
+}
+#endif  // MCC_IN(0)
+
+#if MCC_IN(5)
+hipError_t mcc_attrs_solve(size_t ss) {
+    hipError_t err = hipSuccess;
+    for (hipError_t e : {hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss),
+                         hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss),
+                         hipFuncSetAttribute((const void*)&k_sinv_helper, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss)})
+        if (e != hipSuccess) err = e;
     return err;
 }
 
@@ -4338,24 +4424,27 @@ hipError_t mcc_launch_solve(const SolveArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(a.ctx.m > 30 ? kSolveThreads : 256), mcc_solve_shmem(a.ctx.m), s, a);
     return hipGetLastError();
 }
+hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s) {
+    const size_t shm = mcc_solve_shmem(m);
+    hipError_t e = hipFuncSetAttribute((const void*)&k_debug_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_debug_solve, dim3(1), dim3(kSolveThreads), shm, s, packed, x, m, err, stamps);
+    return hipGetLastError();
+}
 hipError_t mcc_launch_sinv_helper(const WarmCtx& w, int m, int n_systems, hipStream_t s) {
     const size_t M = 16 * (size_t)((m + 15) / 16);
     const size_t shm = (M * (M + 1) + 16 * kBlkLd) * sizeof(double);
     hipLaunchKernelGGL(k_sinv_helper, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
     return hipGetLastError();
 }
+#endif  // MCC_IN(5)
+
+#if MCC_IN(0)
 hipError_t mcc_launch_peer_push(const PeerCtx& pc, const State* st, const double* vals, hipStream_t s) {
     // ~16 KB of words per workgroup: 8 ranks at m = 90 -> 30 workgroups
     const long long bytes = 16LL * pc.Lc * (pc.nranks - 1);
     const int grid = (int)std::min<long long>(64, std::max<long long>(1, (bytes + 16383) / 16384));
     hipLaunchKernelGGL(k_peer_push, dim3(grid), dim3(256), 0, s, pc, st, vals);
-    return hipGetLastError();
-}
-hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* err, long long* stamps, hipStream_t s) {
-    const size_t shm = mcc_solve_shmem(m);
-    hipError_t e = hipFuncSetAttribute((const void*)&k_debug_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_debug_solve, dim3(1), dim3(kSolveThreads), shm, s, packed, x, m, err, stamps);
     return hipGetLastError();
 }
 hipError_t mcc_launch_peer_handshake(const PeerCtx& pc, State* st, double* out, hipStream_t s) {
@@ -4392,3 +4481,4 @@ hipError_t mcc_launch_project_error(const ErrArgs& a, int model, int n_edges, bo
 #undef PE
     return hipGetLastError();
 }
+#endif  // MCC_IN(0)
