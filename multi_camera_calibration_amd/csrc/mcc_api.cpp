@@ -760,9 +760,6 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // and the tilt's per-corner 3 x 3 map and 2 x 2 chain spill there; k_group / k_edge have room)
     const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64 && p->prism != 2;
     p->fused = fusable && V <= 2 * n_cu;
-    if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
-    if (!p->fused && p->max_epp > 64)
-        return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
 
     // ---- Schur pair lists.  The split step's photo work (k_group / k_photo) takes groups of
     // consecutive photos (at most kPhotoGroup photos and the cap's edges) and sums the group's pair
@@ -794,6 +791,14 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     int group_cap = mcc::kGroupRound;   // MCC_GROUP_EDGES: k_group's groups smaller than a round (A/B)
     if (const char* f = std::getenv("MCC_GROUP_EDGES")) group_cap = std::max(1, std::min(mcc::kGroupRound, std::atoi(f)));
     std::vector<int> pgrp_ptr = make_groups(group_cap);
+    // The fused kernel runs a photo's edges one per wave on its four waves, so photos with more than
+    // four edges take it through several dependent rounds; k_group spreads a group's 16 edges over its
+    // eight waves in one.  With more than four edges per photo and k_group's groups within the CUs the
+    // split step wins (config5's 500-view shard, 8 edges per photo: 28.9 vs 32.5 us per step).
+    if (p->fused && p->max_epp > 4 && (int)pgrp_ptr.size() - 1 <= n_cu) p->fused = false;
+    if (const char* f = std::getenv("MCC_FUSED")) p->fused = fusable && std::atoi(f) != 0;
+    if (!p->fused && p->max_epp > 64)
+        return bail(fail(MCC_EINVAL, "more than 64 edges (camera observations) of one photo vertex"));
     p->use_group = !p->fused && (int)pgrp_ptr.size() - 1 <= n_cu;
     if (const char* f = std::getenv("MCC_GROUP")) p->use_group = !p->fused && std::atoi(f) != 0;
     if (!p->use_group) pgrp_ptr = make_groups(mcc::kPhotoGroupEdges);

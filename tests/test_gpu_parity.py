@@ -98,6 +98,10 @@ CASES["config3_small_g32"] = CASES["config3_small"]
 # the three-kernel step's k_prep4 (4 lanes per edge prologue, MCC_PREP_LANES=4; default k_prep, one lane)
 for _n in ["config3_small", "pinhole_back", "config5_small"]:
     CASES[_n + "_prep4"] = CASES[_n]
+# the fused step forced (MCC_FUSED=1) where photos have more than four edges and the split step is
+# the default (DoubleSide: eight cameras see every photo)
+for _n in ["config5_small", "pinhole_back"]:
+    CASES[_n + "_fused"] = CASES[_n]
 
 
 def make_adjuster(name, p):
@@ -112,6 +116,8 @@ def make_adjuster(name, p):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "16"}
     elif name.endswith("_g32"):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "32"}
+    elif name.endswith("_fused"):
+        env = {"MCC_FUSED": "1"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -365,11 +371,12 @@ def _device_cus():
 
 def test_step_path_selection():
     """mcc_create's choice (mcc_problem_path): the fused single-kernel step for m <= 30 with at most
-    two photo workgroups per CU, the split step for more photos or m > 30; MCC_FUSED=0 forces the
-    split step (the *_split cases above).  The photo bound follows the device's CU count."""
+    two photo workgroups per CU, the split step for more photos or m > 30, and for photos with more
+    than four edges whose k_group groups fit the CUs (config5: eight edges per photo); MCC_FUSED=0 / 1
+    force either (the *_split / *_fused cases above).  The photo bound follows the device's CU count."""
     cus = _device_cus()
     cases = [("config2", 2 * cus, "fused"), ("config2", 2 * cus + 64, "split"), ("config3", 40, "split"),
-             ("config5", 60, "fused")]
+             ("config5", 60, "split")]
     for name, views, want in cases:
         p = rig.make_config(name, n_views=views)
         g = api.BundleAdjuster(p)
