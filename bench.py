@@ -172,7 +172,11 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
     per = wins / DIST_STEPS
     dist = {q: ba.allreduce_max(float(np.percentile(per, v))) for q, v in (("p10", 10), ("median", 50), ("p90", 90))}
     step_ms_ev = ba.allreduce_max(float(np.mean(per)))   # graph-launched steps, like the headline
-    if lin_kernels(ba) != "k_linearize":
+    if lin_kernels(ba) == "k_linearize" or ba.folded():
+        # one kernel per step (the fused kernel, or k_group with the reduction and solve folded in):
+        # the kernel's time is the graph-launched step's, as rocprofv3 averages it
+        lin_ms = step_ms_ev
+    else:
         # the split step's linearisation kernels alone, `window` launches in one captured graph
         # between two HIP events (the eager window above puts an event pair between every kernel)
         lin_ms = ba.allreduce_max(ba.timing_linearize(window))
@@ -185,16 +189,18 @@ def measure(ba, steps: int, warmup: int, ramp_s: float, window: int):
 
 def lin_kernels(ba) -> str:
     """The kernels of the linearisation window (mcc_timing_*): the fused kernel, the split step's
-    group kernel, or its three-kernel form (mcc_problem_path says which)."""
-    return ba.step_kernels()
+    group kernel (with the reduction and the m <= 30 solve folded into its launch: the whole step), or
+    its three-kernel form (mcc_problem_path says which)."""
+    return ba.step_kernels() + (" (folded: the whole step)" if ba.folded() else "")
 
 
 def roofline(st, lin_ms, tr=None, kernel="k_linearize"):
     achieved = st["alg_bytes"] / (lin_ms * 1e-3) / 1e9
     return {
-        "kernel_timing": ("HIP events on the step stream around graph launches: the fused kernel (the whole step), "
-                          "a window of graph-launched steps; the split step, a captured graph of its linearisation "
-                          "kernels alone, launched back to back (mcc_timing_linearize)"),
+        "kernel_timing": ("HIP events on the step stream around graph launches: one kernel per step (the fused "
+                          "kernel, or k_group with the reduction and solve folded in), a window of graph-launched "
+                          "steps; the split step, a captured graph of its linearisation kernels alone, launched "
+                          "back to back (mcc_timing_linearize)"),
         "bound": "hbm",
         "kernel": kernel,
         "achieved": achieved,

@@ -227,7 +227,9 @@ int mcc_problem_stats(const mcc_problem *p, long long *corners, long long *edges
                       long long *photos, long long *alg_bytes_per_step);
 /* which step the problem runs: *split_step = 0 for the fused single-kernel step (m <= 30 and at
  * most two photo workgroups per CU, or MCC_FUSED=1), 2 for the split step with its linearisation
- * as one group kernel (k_group, k_schur, [k_solve]), 1 for the split step's three-kernel form
+ * as one group kernel (k_group, k_schur, [k_solve]), 3 for that group kernel with the reduction and
+ * the m <= 30 solve folded into its launch (one k_group launch per step; MCC_GFOLD=0 gives 2), 1 for
+ * the split step's three-kernel form
  * (k_prep, k_edge, k_photo, k_schur, [k_solve]; MCC_GROUP=0); *photo_groups = the groups'
  * workgroups (split step).  The choice
  * depends on the device's CU count (fused iff m <= 30 and n_photos <= 2 x CUs: 512 on MI355X), and

@@ -1578,7 +1578,7 @@ int mcc_timing_exchange(mcc_problem* p, double* ms_per_exchange, int* exchanges)
 
 int mcc_problem_path(const mcc_problem* p, int* split_step, int* photo_groups) {
     if (!p) return fail(MCC_EINVAL, "null problem");
-    if (split_step) *split_step = p->fused ? 0 : (p->use_group ? 2 : 1);
+    if (split_step) *split_step = p->fused ? 0 : (p->use_group ? (p->gfold ? 3 : 2) : 1);
     if (photo_groups) *photo_groups = p->fused ? 0 : p->n_pgroups;
     return MCC_OK;
 }
