@@ -233,6 +233,8 @@ struct mcc_problem {
     // between launches like the slots and the item partials
     bool gfold = false;
     int fold_direct = 0;   // the final workgroup sums where the words land (LinArgs::fold_direct)
+    int fold_dyn = 0;      // the groups take the reduction's tasks as they finish (LinArgs::fold_dyn)
+    DevBuf<int> fold_ticket;
     int max_item_slots = 0;
     DevBuf<double> fnorm, fiv;
     int fault_photo = -1;            // MCC_FAULT_PHOTO (test): LinArgs::fault_photo
@@ -432,6 +434,8 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
         la.fold = 1;
         la.fold_parts = p->n_items + p->n_norm_chunks;
         la.fold_direct = p->fold_direct;
+        la.fold_dyn = p->fold_dyn;
+        la.fold_ticket = p->fold_ticket.p;
         la.fsa = sa;
         la.fsa.ssinv = la.ssinv ? p->fiv.p : nullptr;   // this launch's spare -> the final workgroup
         la.fsa.ssinv_ok = nullptr;
@@ -590,6 +594,8 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     // the fused step's spare protocol restarts (the stream is idle: no spare of an earlier launch runs)
     p->h_state->spare_ack = 0;
     HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
+    // the folded reduction's task ticket (a failed launch's groups may not all have drawn)
+    if (p->fold_ticket.p) HIPCHK(hipMemset(p->fold_ticket.p, 0, sizeof(int)));
     return MCC_OK;
 }
 
@@ -1085,6 +1091,18 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         p->fold_direct = p->group_lanes == 32 && max_bi <= 8 && p->n_norm_chunks <= 4 && ivt > 0 &&
                          p->m * p->m <= 8 * ivt;
         if (const char* f = std::getenv("MCC_FOLD_DIRECT")) p->fold_direct = p->fold_direct && std::atoi(f) != 0;
+        // MCC_FOLD_DYN=1: the groups themselves take the items, norm chunks and the final task by ticket
+        // once their own work is done, instead of trailing workgroups that wait for a CU the groups free
+        // (config5's 500-view shard: the trailing items started 1.5 us after the last group ended).
+        // Measured, not the default: config4 26.55 vs 26.41 us per step, config5's shard 29.3 vs 29.5
+        // (interleaved, gpurun_out/r05u) -- the last group's slots, not the items' start, set the tail.
+        const char* fd = std::getenv("MCC_FOLD_DYN");
+        p->fold_dyn = fd && std::atoi(fd) != 0 && p->n_pgroups >= 2 * (p->n_items + p->n_norm_chunks + 1) &&
+                      p->prism != 2;
+        if (p->fold_dyn) {
+            HIPC(p->fold_ticket.alloc(1));
+            HIPC(hipMemset(p->fold_ticket.p, 0, sizeof(int)));
+        }
         for (auto* b : {&p->pairprod, &p->item_out, &p->fnorm, &p->fiv})
             if (b->p) HIPC(hipMemset(b->p, 0xFF, sizeof(double) * std::max<size_t>(b->n, 1)));
     }
@@ -1145,7 +1163,8 @@ void mcc_destroy(mcc_problem* p) {
     p->cam_pose.release(); p->resid.release(); p->edge_sum.release(); p->corner_err.release(); p->stamps.release();
     p->contrib.release(); p->gsum.release(); p->cnt.release(); p->W.release();
     p->ds_rt.release(); p->Y.release(); p->pairprod.release(); p->zp.release();
-    p->erec.release(); p->echain.release(); p->eh.release(); p->tilt.release(); p->fnorm.release(); p->fiv.release(); p->ssinv.release(); p->ssinv_ok.release();
+    p->erec.release(); p->echain.release(); p->eh.release(); p->tilt.release(); p->fnorm.release(); p->fiv.release();
+    p->fold_ticket.release(); p->ssinv.release(); p->ssinv_ok.release();
     p->gp_tot.release(); p->item_out.release(); p->packed.release(); p->dg.release(); p->delta.release();
     p->photo_norm.release(); p->alpha.release();
     p->photo_ptr.release(); p->photo_corner.release(); p->edge_gblock.release(); p->block_items.release(); p->counter.release(); p->cnt_blk.release();

@@ -704,25 +704,12 @@ __device__ __forceinline__ void fold_final(const LinArgs& la) {
 #ifndef MCC_GROUP_OCC
 #define MCC_GROUP_OCC 2   // k_group workgroups per CU the register budget allows (LDS: ~64 KB each)
 #endif
+// The group's work (phases 0, A, B above); false when the loop has stopped (nothing done).
 template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
-__global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_group(LinArgs a) {
+__device__ __forceinline__ bool group_body(const LinArgs& a) {
     constexpr int NT = kGroupRound * L, EPW = 64 / L;   // threads; edges per wave
-    static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
     const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (a.ssinv && grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
-        extern __shared__ __attribute__((aligned(16))) double smem_spare[];
-        small_inverse(a, smem_spare, false);
-        return;
-    }
-    if (a.fold && grp > a.n_pgroups - (a.ssinv ? 0 : 1)) {   // the folded reduction's workgroups
-        if (st->done) return;
-        const int k = grp - a.n_pgroups - (a.ssinv ? 1 : 0);
-        if (k < a.fsa.n_items) fold_item(a, k);
-        else if (k < a.fold_parts) fold_chunk(a, k - a.fsa.n_items);
-        else fold_final<NT>(a);
-        return;
-    }
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
     const int done = st->done, pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update
@@ -730,7 +717,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     const int ge0 = a.pgrp_edge[grp], gne = a.pgrp_edge[grp + 1] - ge0;   // the group's edges are contiguous
     const int q0 = a.gpair_ptr[grp], nq = a.gpair_ptr[grp + 1] - q0;
     const int c0 = a.gcon_ptr[grp], nc = a.gcon_ptr[grp + 1] - c0;
-    if (done) return;
+    if (done) return false;
     long long* stp = a.stamps ? a.stamps + kStampStride * (size_t)grp : nullptr;   // MCC_DIAG: slots 0..11
     SSTAMP(stp, 0, 0);
     const int C = a.n_cams, m = a.global_dim;
@@ -1261,6 +1248,45 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     __syncthreads();
     SSTAMP(stp, 10, 0);
 #endif
+    return true;
+}
+
+template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
+__global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_group(LinArgs a) {
+    constexpr int NT = kGroupRound * L;
+    static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
+    State* st = a.state;
+    const int grp = blockIdx.x, tid = threadIdx.x;
+    if (a.ssinv && grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
+        extern __shared__ __attribute__((aligned(16))) double smem_spare[];
+        small_inverse(a, smem_spare, false);
+        return;
+    }
+    // the folded reduction's task (item, norm chunk, the final): a trailing workgroup's by its index, or
+    // (fold_dyn) a group's next by ticket once its own work is done -- ONE call site of the task code
+    // per kernel (two made k_group half as large again and config4 1 us slower per step).  (Not in the
+    // tilted sensor's variants: at 256 VGPRs the ticket tail tipped their sweep into a spill; the host
+    // keeps the trailing task workgroups there.)
+    int task;
+    if (a.fold && grp > a.n_pgroups - (a.ssinv ? 0 : 1)) {
+        if (st->done) return;
+        task = grp - a.n_pgroups - (a.ssinv ? 1 : 0);
+    } else {
+        if (!group_body<MODEL, RATIONAL, PRISM, BACK, L>(a) || PRISM == 2 || !a.fold_dyn) return;
+        __shared__ int s_task;
+        __syncthreads();   // the group's LDS is free
+        if (tid == 0) {
+            const int t = __hip_atomic_fetch_add(a.fold_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the last taker resets the ticket for the next launch (every other taker has drawn)
+            if (t == a.n_pgroups - 1) __hip_atomic_store(a.fold_ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_task = t;
+        }
+        __syncthreads();
+        task = s_task;
+    }
+    if (task < a.fsa.n_items) fold_item(a, task);
+    else if (task < a.fold_parts) fold_chunk(a, task - a.fsa.n_items);
+    else if (task == a.fold_parts) fold_final<NT>(a);
 }
 
 // ---------------------------------------------------------------- k_prep4

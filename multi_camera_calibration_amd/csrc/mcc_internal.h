@@ -163,6 +163,9 @@ struct LinArgs {
     // kFoldEmpty back after reading it -- no store drain, ticket or fence on either side.
     int fold, fold_parts;
     int fold_direct;          // the final workgroup sums where the words land (fold_final_direct)
+    int fold_dyn;             // the groups take the reduction's tasks by ticket as they finish (no
+                              // trailing workgroups: those waited for a CU until the groups ended)
+    int* fold_ticket;         // fold_dyn: the tasks' ticket (the last of the n_pgroups takers resets it)
     SchurArgs fsa;            // the reduction (k_schur's arguments: items, slots, partials, packed, solve)
     double* fnorm;            // [4V] per photo ||G||^2, ||x||^2, not-PD flag, pad (the norm chunks' input)
     double* fiv;              // [m^2 + 1] the spare's inverse and its status, +-(iteration + 1) as a double

@@ -4304,7 +4304,7 @@ static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) 
     // + the spare workgroup of the m <= 30 warm solve (small_inverse)
     // (+ the folded reduction's item, norm-chunk and final workgroups)
     hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>),
-                       dim3(a.n_pgroups + (a.ssinv ? 1 : 0) + (a.fold ? a.fold_parts + 1 : 0)),
+                       dim3(a.n_pgroups + (a.ssinv ? 1 : 0) + (a.fold && !a.fold_dyn ? a.fold_parts + 1 : 0)),
                        dim3(kGroupRound * L), shmem, s, a);
     return hipGetLastError();
 }

@@ -288,10 +288,12 @@ def test_folded_group_step_is_bitwise_the_two_kernel_step(views):
     folded consumers poll the hand-off words themselves (kFoldEmpty until written): with the spare
     workgroup held back 300 us (its status word is what the final workgroup waits for before it writes
     the packed system and the state) the bits do not move.  1 000 views is config4 itself (250 groups on
-    256 CUs: the items start only when groups exit).  src/multicalib.cpp:462-514."""
+    256 CUs: the items start only when groups exit).  MCC_FOLD_DYN=1 (the groups take the reduction's
+    tasks by ticket as they finish, no trailing workgroups) gives the same bits.  src/multicalib.cpp:462-514."""
     p = rig.make_config("config4", n_views=views)
     runs = []
-    for env in ({"MCC_GFOLD": "0"}, {}, {"MCC_SPARE_DELAY_US": "300"}):
+    for env in ({"MCC_GFOLD": "0"}, {}, {"MCC_SPARE_DELAY_US": "300"}, {"MCC_FOLD_DYN": "1"},
+                {"MCC_FOLD_DYN": "1", "MCC_SPARE_DELAY_US": "300"}):
         ba = make(p, dict(env, MCC_FUSED="0", MCC_SOLVE_STATS="1"))
         try:
             assert ba.step_kernels() == "k_group"
