@@ -393,6 +393,13 @@ class BundleAdjuster:
         _check(lib().mcc_problem_path(self.h, ctypes.byref(sp), ctypes.byref(ng)), "mcc_problem_path")
         return {0: "k_linearize", 1: "k_prep+k_edge+k_photo", 2: "k_group", 3: "k_group"}[sp.value]
 
+    def photo_groups(self):
+        """The split step's photo-group workgroups (mcc_problem_path; 0 on the fused step)."""
+        sp = ctypes.c_int(0)
+        ng = ctypes.c_int(0)
+        _check(lib().mcc_problem_path(self.h, ctypes.byref(sp), ctypes.byref(ng)), "mcc_problem_path")
+        return ng.value
+
     def folded(self):
         """True when a step is ONE k_group launch: the Schur reduction and the m <= 30 solve folded
         into the group kernel's grid (mcc_problem_path 3; MCC_GFOLD=0 turns it off)."""

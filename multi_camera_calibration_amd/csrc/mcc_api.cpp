@@ -762,6 +762,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     int n_cu = 256;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
+    if (const char* f = std::getenv("MCC_CUS")) n_cu = std::max(1, std::atoi(f));   // test: the path rules at another CU count
     // (the tilted sensor takes the split step: the fused kernel's PRISM variants already hold 256 VGPRs,
     // and the tilt's per-corner 3 x 3 map and 2 x 2 chain spill there; k_group / k_edge have room)
     const bool fusable = p->m <= mcc_problem::kFusedMaxM && V > 0 && p->max_epp <= 64 && p->prism != 2;
@@ -794,9 +795,23 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // k_group (two workgroups per CU) wins while its groups fit the CUs in one wave of workgroups
     // (config4: 32.3 vs 36.9 us per step); with more groups the three-kernel form's higher
     // occupancy wins (config5: 67.3 vs 61.0, config3: 185.5 vs 120.5).  MCC_GROUP=1 / 0 forces.
-    int group_cap = mcc::kGroupRound;   // MCC_GROUP_EDGES: k_group's groups smaller than a round (A/B)
-    if (const char* f = std::getenv("MCC_GROUP_EDGES")) group_cap = std::max(1, std::min(mcc::kGroupRound, std::atoi(f)));
+    int group_cap = mcc::kGroupRound;   // MCC_GROUP_EDGES: k_group's edges per group (A/B; > 16: several rounds)
+    const char* gcap_env = std::getenv("MCC_GROUP_EDGES");
+    if (gcap_env) group_cap = std::max(1, std::min(4 * mcc::kGroupRound, std::atoi(gcap_env)));
     std::vector<int> pgrp_ptr = make_groups(group_cap);
+    // More 16-edge groups than CUs: wider groups (up to two 16-edge rounds each) while that brings them
+    // within one wave of workgroups -- a second wave of groups costs a whole group chain, a second
+    // round inside a group only its edge phases (config3's 8-rank shard, 625 views / 4 871 edges:
+    // 313 groups of 16 -> 244 of <= 24 edges, 58.4 -> 47.4 us per step against the three kernels;
+    // at 64 edges config5's 2 000 views take 65.0 vs 60.2 us, so the widening stops at 32)
+    for (int cap = mcc::kGroupRound + 8; !gcap_env && (int)pgrp_ptr.size() - 1 > n_cu && cap <= 2 * mcc::kGroupRound;
+         cap += 8) {
+        std::vector<int> g = make_groups(cap);
+        if ((int)g.size() - 1 <= n_cu) {
+            pgrp_ptr = std::move(g);
+            group_cap = cap;
+        }
+    }
     // The fused kernel runs a photo's edges one per wave on its four waves, so photos with more than
     // four edges take it through several dependent rounds; k_group spreads a group's 16 edges over its
     // eight waves in one.  With more than four edges per photo and k_group's groups within the CUs the

@@ -102,6 +102,11 @@ for _n in ["config3_small", "pinhole_back", "config5_small"]:
 # the default (DoubleSide: eight cameras see every photo)
 for _n in ["config5_small", "pinhole_back"]:
     CASES[_n + "_fused"] = CASES[_n]
+# k_group's widened groups (two 16-edge rounds per group when 16-edge groups outnumber the CUs; the path
+# rules run at a small MCC_CUS so that a small rig takes them): m = 90 (k_schur -> k_solve), m = 18 folded
+_WIDE_CUS = {"config3": 16, "config4": 6}
+for _n in ["config3_small", "config4_small"]:
+    CASES[_n + "_wide"] = CASES[_n]
 
 
 def make_adjuster(name, p):
@@ -118,6 +123,8 @@ def make_adjuster(name, p):
         env = {"MCC_FUSED": "0", "MCC_GROUP": "1", "MCC_GROUP_LANES": "32"}
     elif name.endswith("_fused"):
         env = {"MCC_FUSED": "1"}
+    elif name.endswith("_wide"):   # (CU counts that make the small rigs' 16-edge groups outnumber them)
+        env = {"MCC_FUSED": "0", "MCC_CUS": str(_WIDE_CUS[name.split("_")[0]])}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -139,10 +146,14 @@ def case(request):
 def test_forced_step_kernels(case):
     """The A/B suffixes reach the linearisation kernels they name (mcc_problem_path)."""
     name, p, o, g = case
-    want = {"_split3": "k_prep+k_edge+k_photo", "_prep4": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group"}
+    want = {"_split3": "k_prep+k_edge+k_photo", "_prep4": "k_prep+k_edge+k_photo", "_g16": "k_group", "_g32": "k_group",
+            "_wide": "k_group"}
     for suf, k in want.items():
         if name.endswith(suf):
             assert g.step_kernels() == k, name
+    if name.endswith("_wide"):   # widened: within the MCC_CUS "CUs", which 16-edge groups would outnumber
+        cus = _WIDE_CUS[name.split("_")[0]]
+        assert g.photo_groups() <= cus < -(-p.n_edges // 16), (name, g.photo_groups(), p.n_edges)
 
 
 def test_residuals_bitwise(case):
