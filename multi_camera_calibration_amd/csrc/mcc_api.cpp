@@ -219,7 +219,9 @@ struct mcc_problem {
     double* sinv = nullptr;          // [M x M] the helper's S^-1 (ordinary memory)
     double* prev2 = nullptr;         // uncached: [2][prev_stride] k_schur's copies of [S | r] (iteration parity)
     int prev_stride = 0;
-    unsigned* wsync = nullptr;       // uncached: [4] epochs, stop; followed by the helper's PD flag
+    unsigned* wsync = nullptr;       // uncached: [8] epochs, stop, the helper's PD flag; its refined epoch, status, corrections
+    double* xsol = nullptr;          // uncached: [128] the helper's solution (helper_refine)
+    bool helper_refine = false;      // single GPU, m > 30: the helper refines too (MCC_HELPER_REFINE)
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
     // k_solve's bound on the wait for the helper (MCC_WARM_TIMEOUT_MS, default 10 s; a step that hits
@@ -307,7 +309,8 @@ mcc::SolveCtx solve_ctx(mcc_problem* p, int do_update) {
 mcc::WarmCtx warm_ctx(mcc_problem* p) {
     const int copy_prev = (p->comm || p->peer_on) ? 1 : 0;   // sharded: k_solve copies the summed system
     return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->prev2, p->prev_stride, copy_prev, p->wsync, p->warm_stats.p,
-                        p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks};
+                        p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks,
+                        p->helper_refine && !copy_prev ? 1 : 0, p->xsol};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
@@ -421,6 +424,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
         sa.one_level = p->schur_one_level;
         sa.prev2 = p->warm && do_update && !p->comm && !p->peer_on ? p->prev2 : nullptr;   // single GPU
         sa.prev_stride = p->prev_stride;
+        sa.wpub = sa.prev2 && p->helper_refine ? p->wsync : nullptr;   // (single GPU: prev2 set)
         sa.ssinv = swarm ? p->ssinv.p : nullptr;
         sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
         sa.peer = peer_ctx(p, peer && !split);
@@ -580,6 +584,7 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
         // batch's helper has exited or will after inverting the last published system: wait for it.
         HIPCHK(hipStreamSynchronize(p->side));
         HIPCHK(hipMemset(p->wsync, 0, 2 * sizeof(unsigned)));
+        HIPCHK(hipMemset(p->wsync + 4, 0, 3 * sizeof(unsigned)));   // the helper's refined epoch, status, corrections
     }
     if (reset_iter) {
         p->h_state->iter = 0;
@@ -1123,6 +1128,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     }
     p->warm = !p->fused && p->m > 30;
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
+    p->helper_refine = p->warm && p->m <= 96;   // (single GPU only: warm_ctx, enqueue_step; the warm path's M <= 96)
+    if (const char* f = std::getenv("MCC_HELPER_REFINE")) p->helper_refine = p->helper_refine && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
     if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
     if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
@@ -1140,8 +1147,10 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         HIPC(hipMalloc((void**)&p->sinv, M * M * sizeof(double)));   // cached: the helper releases it, k_solve reads it in a later launch
         p->prev_stride = (p->ntri + p->m + 1) & ~1;
         HIPC(hipExtMallocWithFlags((void**)&p->prev2, 2 * (size_t)p->prev_stride * sizeof(double), hipDeviceMallocUncached));
-        HIPC(hipExtMallocWithFlags((void**)&p->wsync, 4 * sizeof(unsigned), hipDeviceMallocUncached));
-        HIPC(hipMemset(p->wsync, 0, 4 * sizeof(unsigned)));
+        HIPC(hipExtMallocWithFlags((void**)&p->wsync, 8 * sizeof(unsigned), hipDeviceMallocUncached));
+        HIPC(hipMemset(p->wsync, 0, 8 * sizeof(unsigned)));
+        HIPC(hipExtMallocWithFlags((void**)&p->xsol, 128 * sizeof(double), hipDeviceMallocUncached));
+        HIPC(hipMemset(p->xsol, 0, 128 * sizeof(double)));
         if (!p->warm_stats.p) HIPC(p->warm_stats.alloc(5));
         HIPC(hipMemset(p->warm_stats.p, 0, 5 * sizeof(long long)));
         HIPC(stream_pool().take(d->device, &p->side, true));
@@ -1160,6 +1169,7 @@ void mcc_destroy(mcc_problem* p) {
     if (p->sinv) (void)hipFree(p->sinv);
     if (p->prev2) (void)hipFree(p->prev2);
     if (p->wsync) (void)hipFree(p->wsync);
+    if (p->xsol) (void)hipFree(p->xsol);
     p->warm_stats.release();
     drop_graphs(p);
     p->xsave.release(); p->ysave.release(); p->zpsave.release();

@@ -88,6 +88,8 @@ struct SchurArgs {
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
     double* prev2;       // m > 30 warm solve: [2][prev_stride] copy of [S | r] for the helper (null: off)
     int prev_stride;
+    unsigned* wpub;      // m > 30, the helper refines (WarmCtx::refine): the final arriver publishes the
+                         // system (sync[0] = iteration + 1) as soon as prev2 is complete
 };
 
 struct LinArgs {
@@ -302,7 +304,9 @@ struct WarmCtx {
     int prev_stride;         // packed [S | r] rounded up to even
     int copy_prev;           // 1: k_solve writes the copy (sharded: the rank-summed system exists only
                              // after the exchange); 0: k_schur wrote it (single GPU)
-    unsigned* sync;          // [3] epochs: systems published by k_solve, systems inverted by the helper; stop
+    unsigned* sync;          // [8] epochs: systems published (k_solve; refine: k_schur), systems inverted by the
+                             // helper; stop; PD; refine: the epoch the helper refined, its status (0 no
+                             // inverse, 1 converged, 2 not), its corrections
     long long* stats;        // [5] warm solves, corrections, fallbacks, direct (no inverse yet), waited for the helper
     int poison;              // test (MCC_WARM_POISON=1): the helper publishes a NaN inverse, so every
                              // warm solve must fall back to the direct elimination
@@ -311,6 +315,9 @@ struct WarmCtx {
                              // batch's k_solves publish or raise the stop flag, and the host launches the
                              // helper only after the batch's graphs exist)
     long long delay_ticks;   // test (MCC_WARM_DELAY_US): the helper holds each inverse back this long
+    int refine;              // single GPU (MCC_HELPER_REFINE): the helper refines with the inverse it holds in
+                             // LDS and publishes x (xsol); k_solve only waits for it (or eliminates)
+    double* xsol;            // refine: [kWarmN] uncached, the helper's solution of the published system
 };
 constexpr int kWarmMaxIters = 4;
 

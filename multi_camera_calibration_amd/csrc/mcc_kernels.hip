@@ -2883,7 +2883,13 @@ __device__ __forceinline__ double warm_dot_abs(const double (&a)[kWarmQ], const 
     sa = t;
     return s;
 }
-__device__ __forceinline__ int warm_lc2(int m) { return (m * (m + 1) / 2 + m + 1) / 2; }   // packed [S | r] in double2
+__host__ __device__ __forceinline__ int warm_lc2(int m) { return (m * (m + 1) / 2 + m + 1) / 2; }   // packed [S | r] in double2
+// the helper's LDS: the elimination [M x (M + 1)] and its pivot scratch; refine: the staged [S | r],
+// the solution and warm_refine's work area
+__host__ __device__ __forceinline__ size_t helper_shmem_doubles(int m, bool refine) {
+    const size_t M = 16 * (size_t)((m + 15) / 16);
+    return M * (M + 1) + 16 * kBlkLd + (refine ? 2 * (size_t)warm_lc2(m) + 2 * kWarmN + 8 : 0);
+}
 // LDS doubles of the warm path behind x (kWarmN): packed [S | r] (even length), S^-1 (M x (M + 2)),
 // the residual (kWarmN), wave maxima
 __host__ __device__ __forceinline__ size_t warm_shmem_doubles(int m) {
@@ -2903,10 +2909,12 @@ __device__ __forceinline__ void warm_gather_s(const double* Pk, int m, double (&
         Sr[c] = row && g * kWarmQ + c < m ? v : 0.0;
     }
 }
-// the refinement: Sr (registers), Iv = S_t^-1 (LDS, M + 2 stride), Pk = packed [S | r] (LDS);
-// x[kWarmN] receives the solution (zero beyond m)
-__device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const double* Pk, double* x, double* work,
-                            int m, long long* stats) {
+// the refinement: Sr (registers), Iv = S_t^-1 (LDS, row stride ivld: k_solve's M + 2, the helper's
+// elimination layout M + 1), Pk = packed [S | r] (LDS); x[kWarmN] receives the solution (zero beyond
+// m).  stats (k_solve): the counters; corr (the helper): the corrections run
+template <bool ODD_LD>
+__device__ __forceinline__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, int ivld, const double* Pk,
+                                            double* x, double* work, int m, long long* stats, int* corr = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     constexpr int nw = kSolveThreads / 64;
     const int i = tid >> 2, g = tid & 3;
@@ -2915,12 +2923,20 @@ __device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const 
     const bool row = i < m;
     const int ic = row ? i : 0;
     double Ir[kWarmQ];
+    if (!ODD_LD) {   // 16-B aligned rows
 #pragma unroll
-    for (int c = 0; c < kWarmQ; c += 2) {
-        const int j = g * Qp + c;
-        const double2 v = *reinterpret_cast<const double2*>(Iv + ic * (M + 2) + min(j, M - 2));
-        Ir[c] = row && j < m ? v.x : 0.0;
-        Ir[c + 1] = row && j + 1 < m ? v.y : 0.0;
+        for (int c = 0; c < kWarmQ; c += 2) {
+            const int j = g * Qp + c;
+            const double2 v = *reinterpret_cast<const double2*>(Iv + ic * ivld + min(j, M - 2));
+            Ir[c] = row && j < m ? v.x : 0.0;
+            Ir[c + 1] = row && j + 1 < m ? v.y : 0.0;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < kWarmQ; ++c) {
+            const int j = g * Qp + c;
+            Ir[c] = row && j < m ? Iv[ic * ivld + j] : 0.0;
+        }
     }
     const double rr = row ? Pk[ntri + i] : 0.0;
     double* rv = work;            // [nv] right-hand side, then the residual
@@ -2965,11 +2981,12 @@ __device__ bool warm_refine(const double (&Sr)[kWarmQ], const double* Iv, const 
         xi += warm_dot(Ir, rv + g * Qp);
         ++it;
     }
-    if (tid == 0) {
+    if (tid == 0 && stats) {
         stats[0] += 1;
         stats[1] += it;
         if (!conv) stats[2] += 1;
     }
+    if (corr) *corr = it;
     return conv;
 }
 // The warm buffers are uncached device memory: plain loads and stores go to HBM whatever their
@@ -2982,6 +2999,13 @@ __device__ __forceinline__ void st_sys_x2(double* p, double a, double b) {
     v.x = a;
     v.y = b;
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");   // (st_sc1_x2's hazard)
+}
+// prev2 in the resident helper: system-scope loads.  Plain loads of the uncached buffer were served
+// stale copies in a helper that runs for many systems (round 5: the previous use of the same parity
+// buffer, two systems back -- every refinement with the carried inverse then fell back)
+__device__ __forceinline__ double ld_sys_f64(const double* p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
 }
 __device__ __forceinline__ unsigned ld_sys_u32(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3023,6 +3047,27 @@ __device__ __forceinline__ void warm_issue(const double* packed, int m, WarmStag
 // helper found the last one not positive definite -- both functions of the systems alone), -1 the
 // helper did not deliver within wait_ticks (the step fails: kErrWarmTimeout)
 __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigned* e_s) {
+    if (w.refine) {
+        // the helper solves: wait for its solution of the system k_schur published (epoch e); 2: use
+        // it, 0: eliminate (no inverse of the previous system, or the refinement did not converge)
+        const unsigned e = ld_sys_u32(w.sync);
+        uint4 hy = *reinterpret_cast<const uint4*>(w.sync + 4);   // {solved epoch, status, corrections, -}
+        if (hy.x != e) {
+            w.stats[4] += 1;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (hy.x != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < w.wait_ticks) {
+                __builtin_amdgcn_s_sleep(2);
+                hy.x = ld_sys_u32(w.sync + 4);
+            }
+            hy.y = ld_sys_u32(w.sync + 5);
+            hy.z = ld_sys_u32(w.sync + 6);
+        }
+        // use: -1 the helper did not deliver; else (corrections << 3) | (0 no inverse, 1 refined, not
+        // converged, 2 converged: x is the helper's); counted by warm_finish, when the solve is used
+        *use_s = hy.x == e ? (int)((hy.z << 3) | (hy.y == 0u ? 0u : hy.y == 1u ? 2u : 1u)) : -1;
+        *e_s = e;
+        return;
+    }
     const uint4 sy = *reinterpret_cast<const uint4*>(w.sync);   // {published, inverted, stop, PD}
     const unsigned e = sy.x;
     unsigned h = sy.y, ok = sy.w;
@@ -3052,6 +3097,28 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
     double* Iv = Pk + 2 * n2;                        // staged S_t^-1
     double* work = Iv + (size_t)M * (M + 2);
     double* prev = w.prev2 + (size_t)(e & 1u) * w.prev_stride;   // iteration e's copy
+    if (w.refine) {   // the helper's solution (use 2), else the direct elimination; k_schur published
+        if (tid == 0) {
+            if ((use & 7) == 0) {
+                w.stats[3] += 1;
+            } else {
+                w.stats[0] += 1;
+                w.stats[1] += use >> 3;
+                if ((use & 7) == 1) w.stats[2] += 1;
+            }
+        }
+        if ((use & 7) == 2) {
+            for (int t = tid; t < kWarmN; t += blockDim.x)
+                x[t] = t < m ? __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<unsigned long long*>(w.xsol + t),
+                                                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                             : 0.0;
+            lds_barrier();
+        } else {
+            gj_blocked(packed, x, x + M, x + M + M * (M + 1), m, err, nullptr, bad_lds);
+        }
+        SSTAMP(stp, 11, 0);
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kWarmPer; ++u) {
         const int q = u * (int)blockDim.x + tid;
@@ -3094,7 +3161,7 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
         lds_barrier();
         if (early && tid == 0) st_sys_u32(w.sync, e + 1u);
         SSTAMP(stp, 9, 0);   // S_t^-1 in LDS, the rows of S_{t+1} gathered
-        solved = warm_refine(Sr, Iv, Pk, x, work, m, w.stats);
+        solved = warm_refine<false>(Sr, Iv, M + 2, Pk, x, work, m, w.stats);
         SSTAMP(stp, 10, 0);   // refined
     }
     if (!solved) gj_blocked(packed, x, x + M, x + M + M * (M + 1), m, err, nullptr, bad_lds);
@@ -3154,14 +3221,47 @@ __device__ bool gj_inverse_blocked(double* A, double* PV, int M) {
 // stopped, a failed step, a peer timeout), or after kHelperIdleTicks without a new system: every
 // wave reaches the exit.
 #if MCC_IN(5)
+// With WarmCtx::refine (single GPU) the helper also SOLVES each system: k_schur's final arriver
+// publishes the system as soon as its copy in prev2 is complete (sync[0] = iteration + 1), the helper
+// stages it, refines with the inverse of the previous system it still holds in LDS (the same
+// warm_refine, the same bits k_solve would form), publishes x (xsol, then sync[5] status, sync[6]
+// corrections, sync[4] = the epoch) and only then inverts the new system in place.  k_solve waits for
+// sync[4] instead of loading S_t^-1 (74 KB) and refining: 3.1 + 3.4 us of its 10.5 us at m = 90
+// (tools/diag_solve.py), which now run while k_schur ends and k_solve starts.  The refinement runs
+// only with the inverse of system e - 1 (a batch's helper starts from sinv and the epoch sync[1]
+// names), so its branch is a function of the systems alone, as before.
 __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m, int n_systems) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ unsigned ep_s;
-    __shared__ int quit_s;
+    __shared__ int quit_s, have_s;
     const int tid = threadIdx.x, M = 16 * ((m + 15) / 16), ld = M + 1;
     double* A = sm;
     double* PV = sm + M * ld;
+    const int n2 = warm_lc2(m);
+    double* Pk = PV + 16 * kBlkLd;   // refine: the staged packed [S | r] (even length)
+    double* xs = Pk + 2 * n2;        // refine: the solution [kWarmN]
+    double* work = xs + kWarmN;      // refine: warm_refine's residual and wave maxima
     unsigned seen = ld_sys_u32(w.sync + 1);
+    unsigned held = 0u;   // refine: the epoch whose inverse A holds
+    // A -> sinv (ordinary, cached memory: this XCD's L2 written back before an epoch says it is there;
+    // its readers run in later launches, whose start drops stale lines from their own caches)
+    auto dump_inverse = [&]() {
+        for (int q = tid; q < M * M / 2; q += blockDim.x) {
+            const int t = 2 * q, i = t / M, j = t % M;
+            *reinterpret_cast<double2*>(w.sinv + t) =
+                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(A[i * ld + j], A[i * ld + j + 1]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    };
+    if (w.refine) {
+        // the inverse the previous batch's helper left (sinv, for epoch sync[1], positive definite)
+        const bool have = seen != 0u && ld_sys_u32(w.sync + 3) != 0u;
+        if (have) {
+            for (int t = tid; t < M * M; t += blockDim.x) A[(t / M) * ld + t % M] = w.sinv[t];
+            held = seen;
+        }
+        if (tid == 0) have_s = have;
+    }
     for (int k = 0; k < n_systems; ++k) {
         if (tid == 0) {
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -3179,23 +3279,76 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
             quit_s = quit;
         }
         __syncthreads();
-        if (quit_s) return;
+        if (quit_s) {
+            if (w.refine && held != 0u) {   // the next batch's helper starts from it (sync[1], sync[3])
+                dump_inverse();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            return;
+        }
         const unsigned e = ep_s;
         // system e (solved by the update step whose iteration counter was e - 1: k_schur wrote it to
         // prev2[(e - 1) & 1]) -> the full symmetric matrix in LDS (padding: identity)
-        const int ntri = m * (m + 1) / 2, n2 = (ntri + 1) / 2;
+        const int ntri = m * (m + 1) / 2;
         const double* src = w.prev2 + (size_t)((e - 1u) & 1u) * w.prev_stride;
-        for (int q = tid; q < n2; q += blockDim.x) {
-            const double2 v = ld_sys_x2(src + 2 * q);
-            for (int h = 0; h < 2; ++h) {
-                const int t = 2 * q + h;
-                if (t < ntri) {
-                    int i, j;
-                    packed_ij(t, m, i, j);
-                    const double x = h ? v.y : v.x;
-                    A[i * ld + j] = x;
-                    A[j * ld + i] = x;
-                }
+        if (w.refine) {
+            // [S | r] staged, x = S^-1 r refined with the held inverse of system e - 1, published
+            for (int q = tid; q < 2 * n2; q += blockDim.x) Pk[q] = ld_sys_f64(src + q);
+            __syncthreads();
+            int status = 0, corr = 0;
+#ifdef MCC_HELPER_RELOAD   // (A/B debug builds only)
+            if (have_s && held == e - 1u) {
+                for (int t = tid; t < M * M; t += blockDim.x) A[(t / M) * ld + t % M] = w.sinv[t];
+                __syncthreads();
+            }
+#endif
+#ifdef MCC_HELPER_BARRIER   // (A/B debug builds only)
+            __syncthreads();
+#endif
+            if (have_s && held == e - 1u) {
+                // (m and the LDS bases re-derived per system: hoisted out of the system loop, the
+                // refinement's addresses held ~160 SGPRs for the whole kernel and spilled)
+                int mo = m;
+                asm volatile("" : "+s"(mo));
+                const int Mo = 16 * ((mo + 15) / 16), ldo = Mo + 1;
+                double* Ao = sm;
+                double* Pko = sm + Mo * ldo + 16 * kBlkLd;
+                double* xso = Pko + 2 * warm_lc2(mo);
+                double Sr[kWarmQ];
+                warm_gather_s(Pko, mo, Sr);
+                const bool conv = warm_refine<true>(Sr, Ao, ldo, Pko, xso, xso + kWarmN, mo, nullptr, &corr);
+                status = conv && !w.poison ? 1 : 2;   // (test: a poisoned helper's solves all fall back)
+            }
+            if (status == 1)
+                for (int t = tid; t < m; t += blockDim.x)
+                    __hip_atomic_store(reinterpret_cast<unsigned long long*>(w.xsol + t), (unsigned long long)__double_as_longlong(xs[t]),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0 && w.delay_ticks > 0) {   // test: a slow helper (k_solve must wait, not switch)
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < w.delay_ticks) __builtin_amdgcn_s_sleep(8);
+            }
+            if (tid == 0) {
+                st_sys_u32(w.sync + 5, (unsigned)status);
+                st_sys_u32(w.sync + 6, (unsigned)corr);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sys_u32(w.sync + 4, e);
+            }
+            for (int t = tid; t < ntri; t += blockDim.x) {
+                int i, j;
+                packed_ij(t, m, i, j);
+                const double x = Pk[t];
+                A[i * ld + j] = x;
+                A[j * ld + i] = x;
+            }
+        } else {
+            for (int t = tid; t < ntri; t += blockDim.x) {
+                int i, j;
+                packed_ij(t, m, i, j);
+                const double x = ld_sys_f64(src + t);
+                A[i * ld + j] = x;
+                A[j * ld + i] = x;
             }
         }
         for (int t = tid; t < M * M; t += blockDim.x) {
@@ -3204,23 +3357,32 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         }
         __syncthreads();
         const bool ok = gj_inverse_blocked(A, PV, M);
-        for (int q = tid; q < M * M / 2; q += blockDim.x) {
-            const int t = 2 * q, i = t / M, j = t % M;
-            *reinterpret_cast<double2*>(w.sinv + t) =
-                w.poison ? make_double2(__builtin_nan(""), __builtin_nan("")) : make_double2(A[i * ld + j], A[i * ld + j + 1]);
-        }
-        if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
-        // sinv is ordinary (cached) memory: write this XCD's L2 back before the epoch says it is there
-        // (k_solve reads it in a later launch, whose start drops stale lines from its own caches)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#ifdef MCC_HELPER_RELOAD
+        dump_inverse();
+#else
+        if (!w.refine) dump_inverse();   // (refine: the inverse stays in LDS; sinv only when the helper exits)
+#endif
+#ifdef MCC_HELPER_RELOAD_END   // (A/B debug builds only)
+        dump_inverse();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0 && w.delay_ticks > 0) {   // test: a slow helper (k_solve must wait, not switch)
+        for (int t = tid; t < M * M; t += blockDim.x) A[(t / M) * ld + t % M] = w.sinv[t];
+#endif
+        if (tid == 0) st_sys_u32(reinterpret_cast<unsigned*>(w.sinv_ok_sys), ok ? 1u : 0u);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (!w.refine && tid == 0 && w.delay_ticks > 0) {   // test: a slow helper (k_solve must wait, not switch)
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < w.delay_ticks) __builtin_amdgcn_s_sleep(8);
         }
         if (tid == 0) st_sys_u32(w.sync + 1, e);
         seen = e;
+        held = e;
+        if (tid == 0) have_s = ok;   // (read after the next system's barrier)
+    }
+    if (w.refine && held != 0u) {
+        dump_inverse();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
 #endif  // MCC_IN(5)
@@ -3423,7 +3585,7 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
     __shared__ int s_sm_ok, s_sm_corr;   // m <= 30: the refinement converged, with this many corrections
     __shared__ double s_rv[32];          // m <= 30: the refinement's vector exchange
     WarmStage ws;
-    if (wrm) warm_issue(S, m, ws);
+    if (wrm && !warm->refine) warm_issue(S, m, ws);
     if (wrm && tid == 64) warm_check(*warm, &s_use, &s_ep);
     if (tid == 0) {
         // the error bits the step's photo work set (bit 0), read with the state so that the stop
@@ -3876,6 +4038,10 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
         v = photo_flag_norm(err_now, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
+    } else if (tid == 64 && a.wpub) {
+        // the helper solves this system (WarmCtx::refine): prev2[iter & 1] is complete (the blocks'
+        // sc1 stores drained before their tickets), so publish it now, not from k_solve
+        st_sys_u32(a.wpub, (unsigned)iter_e + 1u);
     }
     if (!a.fuse_solve) return;
     if (a.peer.nranks > 0) {
@@ -4293,7 +4459,8 @@ size_t mcc_solve_shmem(int m) {
     const size_t M = 16 * (size_t)((m + 15) / 16);
     const size_t blocked = M + M * (M + 1) + 2 * 16 * kBlkLd;   // gj_blocked (m > 30, k_solve)
     const size_t warm = M <= kWarmN ? kWarmN + warm_shmem_doubles(m) : 0;   // warm_finish
-    return std::max((size_t)(m * m + m), m > 30 ? std::max(blocked, warm) : 0) * sizeof(double);
+    const size_t helper = M <= kWarmN ? helper_shmem_doubles(m, true) : 0;   // k_sinv_helper (refine)
+    return std::max((size_t)(m * m + m), m > 30 ? std::max(std::max(blocked, warm), helper) : 0) * sizeof(double);
 }
 
 #endif  // MCC_IN(0)
@@ -4432,8 +4599,7 @@ hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* e
     return hipGetLastError();
 }
 hipError_t mcc_launch_sinv_helper(const WarmCtx& w, int m, int n_systems, hipStream_t s) {
-    const size_t M = 16 * (size_t)((m + 15) / 16);
-    const size_t shm = (M * (M + 1) + 16 * kBlkLd) * sizeof(double);
+    const size_t shm = helper_shmem_doubles(m, w.refine != 0) * sizeof(double);
     hipLaunchKernelGGL(k_sinv_helper, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
     return hipGetLastError();
 }

@@ -145,6 +145,34 @@ def test_delayed_helper_is_bitwise_the_undelayed_run():
         assert st0[k] == st1[k], (st0, st1)
 
 
+@pytest.mark.parametrize("name", ["config3_small", "m48"])
+def test_helper_refinement_is_bitwise_k_solves(name):
+    """Single GPU: the helper refines with the inverse it holds in LDS and k_solve only waits for its
+    solution (default; MCC_HELPER_REFINE=0: k_solve loads the inverse and refines itself).  The same
+    warm_refine on the same system and the same inverse: the optimize, the free-running steps and
+    the solve statistics are bitwise / exactly those of the k_solve form."""
+    p = CASES[name]()
+    out = []
+    for env in ({"MCC_HELPER_REFINE": "0"}, {}):
+        ba = make(p, env)
+        try:
+            x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+            ba.set_params(p.x0)
+            ba.step(24)
+            ba.check()
+            xs = ba.get_params()
+            st = ba.solve_stats()
+        finally:
+            ba.close()
+        out.append((x, it, xs, st))
+    (x0, it0, xs0, st0), (x1, it1, xs1, st1) = out
+    assert it0 == it1
+    assert np.array_equal(x0, x1) and np.array_equal(xs0, xs1)
+    for k in ("warm", "corrections", "fallbacks", "direct"):
+        assert st0[k] == st1[k], (st0, st1)
+    assert st1["warm"] > 0
+
+
 def test_helper_timeout_fails_the_step():
     """A helper slower than MCC_WARM_TIMEOUT_MS: the step fails with MCC_ETIMEOUT (-6) instead of
     switching algorithms, and the problem recovers on the next optimisation."""
