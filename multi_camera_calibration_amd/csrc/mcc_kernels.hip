@@ -2994,6 +2994,21 @@ __device__ __forceinline__ bool warm_refine(const double (&Sr)[kWarmQ], const do
 // and written with system-scope atomics so the spin loops re-load them.  The data loads follow
 // the epoch check through a workgroup barrier.
 __device__ __forceinline__ double2 ld_sys_x2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+// 5 x 16 bytes past every cache (sc0 sc1), all in flight before one wait: the resident helper's staging
+// of prev2 (plain loads of the uncached buffer were served stale copies, see ld_sys_f64)
+__device__ __forceinline__ void ld_nc_x2_5(const double* p0, const double* p1, const double* p2, const double* p3,
+                                           const double* p4, f64x2_t (&v)[5]) {
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off sc0 sc1\n\t"
+        "global_load_dwordx4 %1, %6, off sc0 sc1\n\t"
+        "global_load_dwordx4 %2, %7, off sc0 sc1\n\t"
+        "global_load_dwordx4 %3, %8, off sc0 sc1\n\t"
+        "global_load_dwordx4 %4, %9, off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4])
+        : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4)
+        : "memory");
+}
 __device__ __forceinline__ void st_sys_x2(double* p, double a, double b) {
     f64x2_t v;
     v.x = a;
@@ -3293,7 +3308,18 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         const double* src = w.prev2 + (size_t)((e - 1u) & 1u) * w.prev_stride;
         if (w.refine) {
             // [S | r] staged, x = S^-1 r refined with the held inverse of system e - 1, published
-            for (int q = tid; q < 2 * n2; q += blockDim.x) Pk[q] = ld_sys_f64(src + q);
+            for (int q0 = 0; q0 < n2; q0 += 5 * (int)blockDim.x) {   // (n2 <= 2 093 at m = 90: one pass of 512 x 5)
+                const double* pq[5];
+#pragma unroll
+                for (int u = 0; u < 5; ++u) pq[u] = src + 2 * min(q0 + u * (int)blockDim.x + tid, n2 - 1);
+                f64x2_t v[5];
+                ld_nc_x2_5(pq[0], pq[1], pq[2], pq[3], pq[4], v);
+#pragma unroll
+                for (int u = 0; u < 5; ++u) {
+                    const int q = q0 + u * (int)blockDim.x + tid;
+                    if (q < n2) reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
+                }
+            }
             __syncthreads();
             int status = 0, corr = 0;
 #ifdef MCC_HELPER_RELOAD   // (A/B debug builds only)
