@@ -180,8 +180,20 @@ int mcc_peer_enable(mcc_problem *p, int on);
  * (m > 96, MCC_WARM=0, MCC_SMALL_WARM=0, RCCL on the fused step).  Which solve a step takes depends on
  * the systems only, never on timing. */
 int mcc_solve_stats(mcc_problem *p, long long *out);
+/* the last mcc_optimize as its caller saw it: host_ms[4] = {setup (parameters in, state reset), steps
+ * (graph launches of kGraphSteps = 8 steps and the host's stop-test poll after each), finish (the
+ * pending photo update flushed, parameters out), the whole call} in wall milliseconds; *device_ms =
+ * HIP events from before the first step launch to after the last launched step; *launched = steps
+ * launched (the ones after the stop test fired return at once); *iters = updates made; *polls = host
+ * round trips to the stop test. */
+int mcc_optimize_profile(mcc_problem *p, double *host_ms, double *device_ms, int *launched, int *iters,
+                         int *polls);
 /* per-corner float32 residuals fl32(obs - proj) at x, reference corner order [2*corners] */
 int mcc_debug_residuals(mcc_problem *p, const float *x, float *res);
+/* test only: the warm solves' injected delays and wait bound, as MCC_SPARE_DELAY_US / MCC_WARM_DELAY_US /
+ * MCC_WARM_TIMEOUT_MS set them at mcc_create (a negative argument keeps the current value); the captured
+ * step graphs are rebuilt.  Lets a test fail a step by a timeout and then run the same handle again. */
+int mcc_debug_delays(mcc_problem *p, double spare_delay_us, double warm_delay_us, double warm_timeout_ms);
 /* test / measurement: the m > 30 dense solve alone (k_solve's elimination), x = S^-1 r for a
  * packed SPD system [S upper triangle row-major, m(m+1)/2 | r, m] on `device`; with reps > 0 the
  * average device time of `reps` back-to-back launches (one workgroup each) in *us_per_solve; with

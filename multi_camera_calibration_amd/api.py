@@ -108,6 +108,11 @@ def lib():
         L.mcc_check.argtypes = [ctypes.c_void_p]
         L.mcc_project_error.argtypes = [ctypes.c_void_p, _f32p, _f32p, _f64p]
         L.mcc_debug_residuals.argtypes = [ctypes.c_void_p, _f32p, _f32p]
+        # (round-6 entry points: absent from an older build loaded through MCC_LIB for an A/B)
+        if hasattr(L, "mcc_optimize_profile"):
+            L.mcc_optimize_profile.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p, _i32p, _i32p]
+        if hasattr(L, "mcc_debug_delays"):
+            L.mcc_debug_delays.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_double]
         L.mcc_timing_begin.argtypes = [ctypes.c_void_p]
         L.mcc_timing_end.argtypes = [ctypes.c_void_p, _f64p, _f64p, _i32p]
         L.mcc_timing_exchange.argtypes = [ctypes.c_void_p, _f64p, _i32p]
@@ -317,6 +322,22 @@ class BundleAdjuster:
         r = np.zeros(2 * self.prob.n_corners, np.float32)
         _check(lib().mcc_debug_residuals(self.h, _ptr(x, _f32p), _ptr(r, _f32p)), "mcc_debug_residuals")
         return r
+
+    def optimize_profile(self):
+        """The last optimize_extrinsics as the caller saw it (mcc_optimize_profile): host phases (ms),
+        device ms from the first step launch to the end of the last, steps launched, updates, polls."""
+        hm = np.zeros(4, np.float64)
+        dev = ctypes.c_double(0)
+        n, it, polls = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().mcc_optimize_profile(self.h, _ptr(hm, _f64p), ctypes.byref(dev), ctypes.byref(n),
+                                          ctypes.byref(it), ctypes.byref(polls)), "mcc_optimize_profile")
+        return {"host_setup_ms": hm[0], "host_steps_ms": hm[1], "host_finish_ms": hm[2], "host_call_ms": hm[3],
+                "device_ms": dev.value, "steps_launched": n.value, "iters": it.value, "stop_polls": polls.value}
+
+    def debug_delays(self, spare_delay_us=-1.0, warm_delay_us=-1.0, warm_timeout_ms=-1.0):
+        """test only: change the injected warm-solve delays / wait bound of this handle (-1 keeps one)"""
+        _check(lib().mcc_debug_delays(self.h, float(spare_delay_us), float(warm_delay_us), float(warm_timeout_ms)),
+               "mcc_debug_delays")
 
     def timing_begin(self):
         _check(lib().mcc_timing_begin(self.h), "mcc_timing_begin")

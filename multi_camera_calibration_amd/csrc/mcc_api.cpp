@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -236,6 +237,7 @@ struct mcc_problem {
     bool gfold = false;
     int fold_direct = 0;   // the final workgroup sums where the words land (LinArgs::fold_direct)
     int fold_dyn = 0;      // the groups take the reduction's tasks as they finish (LinArgs::fold_dyn)
+    int fold_first = 0;    // MCC_FOLD_CONSUMERS_FIRST=1 (test): LinArgs::fold_first
     DevBuf<int> fold_ticket;
     int max_item_slots = 0;
     DevBuf<double> fnorm, fiv;
@@ -245,6 +247,7 @@ struct mcc_problem {
     DevBuf<int4> edge_info, items, gpairs;
     DevBuf<State> state;
     State* h_state = nullptr;   // pinned staging
+    float* h_x = nullptr;       // [P] pinned staging of mcc_optimize's parameters (allocated on first use)
     int packed_len = 0, ntri = 0;
 
     // graphs: gexec[k] = 2^k update steps (k < kGraphSizes), built on first use; a run of n steps
@@ -296,6 +299,13 @@ struct mcc_problem {
     int ev_x_used = 0;
     long long xchg_ticks0 = 0;
     unsigned xchg_epoch0 = 0;
+    // the last mcc_optimize, as its caller sees it (mcc_optimize_profile): host phases, the device time
+    // from the first step launch to the end of the last, the steps launched, the host's stop-test polls
+    hipEvent_t ev_opt[2] = {nullptr, nullptr};
+    double opt_host_ms[4] = {0, 0, 0, 0};   // setup (parameters in, state), steps (launch + stop polls), finish, call
+    double opt_dev_ms = 0.0;
+    int opt_launched = 0, opt_iters = 0, opt_polls = 0;
+
 };
 
 namespace {
@@ -440,6 +450,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
         la.fold_direct = p->fold_direct;
         la.fold_dyn = p->fold_dyn;
         la.fold_ticket = p->fold_ticket.p;
+        la.fold_first = p->fold_first;
         la.fsa = sa;
         la.fsa.ssinv = la.ssinv ? p->fiv.p : nullptr;   // this launch's spare -> the final workgroup
         la.fsa.ssinv_ok = nullptr;
@@ -578,6 +589,14 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     p->stepping = false;
     HIPCHK(hipStreamSynchronize(p->stream));
     HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
+    if (p->gfold && p->h_state->error) {
+        // a folded launch that failed (a consumer's poll bound, a peer timeout) may have left words
+        // behind: slots its items cleared before a late producer wrote them, partials its final never
+        // read, a late spare's inverse and status.  Every launch of the stream has ended (synchronised
+        // above), so all of them go back to kFoldEmpty, as mcc_create leaves them.
+        for (auto* b : {&p->pairprod, &p->item_out, &p->fnorm, &p->fiv})
+            if (b->p) HIPCHK(hipMemset(b->p, 0xFF, sizeof(double) * std::max<size_t>(b->n, 1)));
+    }
     if (reset_iter && p->warm) {
         // a new optimisation starts without a previous inverse (its first solve is the direct
         // elimination), so its result does not depend on what the problem solved before.  The last
@@ -601,6 +620,41 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
     HIPCHK(hipMemcpy(p->state.p, p->h_state, sizeof(State), hipMemcpyHostToDevice));
     // the folded reduction's task ticket (a failed launch's groups may not all have drawn)
     if (p->fold_ticket.p) HIPCHK(hipMemset(p->fold_ticket.p, 0, sizeof(int)));
+    return MCC_OK;
+}
+
+// mcc_optimize's start: mcc_set_params + set_state(reset) with one host round trip (the state read
+// that tells a failed previous launch and keeps the device-monotonic words); the parameters and the
+// new state go in as copies ordered before the first step on the stream (round 6: the setup took
+// ~8 synchronous copies, ~75 us of a config4 call)
+int begin_optimize(mcc_problem* p, const float* x, int crit_type, int max_count, double eps) {
+    p->stepping = false;
+    if (!p->h_x) HIPCHK(hipHostMalloc((void**)&p->h_x, sizeof(float) * std::max(p->P, 1), hipHostMallocDefault));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    HIPCHK(hipMemcpy(p->h_state, p->state.p, sizeof(State), hipMemcpyDeviceToHost));
+    if (p->gfold && p->h_state->error)   // (set_state: what a failed folded launch leaves)
+        for (auto* b : {&p->pairprod, &p->item_out, &p->fnorm, &p->fiv})
+            if (b->p) HIPCHK(hipMemset(b->p, 0xFF, sizeof(double) * std::max<size_t>(b->n, 1)));
+    if (p->warm) {   // (set_state: no previous inverse; the last batch's helper has exited)
+        HIPCHK(hipStreamSynchronize(p->side));
+        HIPCHK(hipMemset(p->wsync, 0, 2 * sizeof(unsigned)));
+        HIPCHK(hipMemset(p->wsync + 4, 0, 3 * sizeof(unsigned)));
+    }
+    State* h = p->h_state;
+    h->iter = 0;
+    h->change = 1.0;
+    h->cam_normG2 = h->cam_normX2 = 0.0;
+    h->done = 0;
+    h->crit_type = crit_type;
+    h->max_count = max_count;
+    h->eps = eps;
+    h->error = 0;
+    h->spare_ack = 0;
+    h->pending = 0;   // new parameters: no pending photo update
+    std::memcpy(p->h_x, x, sizeof(float) * p->P);
+    HIPCHK(hipMemcpyAsync(p->x.p, p->h_x, sizeof(float) * p->P, hipMemcpyHostToDevice, p->stream));
+    HIPCHK(hipMemcpyAsync(p->state.p, h, sizeof(State), hipMemcpyHostToDevice, p->stream));
+    if (p->fold_ticket.p) HIPCHK(hipMemsetAsync(p->fold_ticket.p, 0, sizeof(int), p->stream));
     return MCC_OK;
 }
 
@@ -767,6 +821,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     int n_cu = 256;
     if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->device) != hipSuccess || n_cu <= 0)
         n_cu = 256;
+    const int n_cu_dev = n_cu;   // the device's own (the folded step's progress rule below)
     if (const char* f = std::getenv("MCC_CUS")) n_cu = std::max(1, std::atoi(f));   // test: the path rules at another CU count
     // (the tilted sensor takes the split step: the fused kernel's PRISM variants already hold 256 VGPRs,
     // and the tilt's per-corner 3 x 3 map and 2 x 2 chain spill there; k_group / k_edge have room)
@@ -1095,7 +1150,19 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     // slots (every m <= 30 rig with several camera-pair blocks takes 64; a one-block rig 320: no fold)
     p->gfold = !p->fused && p->use_group && p->schur_one_level && p->max_item_slots <= 5 * 13 &&
                48 * (p->n_items + p->n_norm_chunks) + p->m * p->m + 1 <= mcc::kSchurOneLevelLoads * 256;
+    // Progress of the folded launch does not rest on dispatch order.  Its producers (the groups, the
+    // spare) never wait; its consumers (items, norm chunks, the final workgroup) spin until their words
+    // land.  Whatever order the dispatcher picks, the launch completes as long as the spinning
+    // consumers cannot hold every workgroup slot a producer needs: with at least one slot left over,
+    // some producer is always resident or dispatchable, runs to its end and frees its slot.  k_group
+    // fits at least one workgroup per CU, so the fold is taken only when the consumers fill at most
+    // half of the CUs (the other half stays for producers even when another kernel shares the device);
+    // otherwise the step is k_group -> k_schur.  MCC_FOLD_CONSUMERS_FIRST=1 (tests) lays the grid out
+    // with the consumers at the lowest indices to exercise exactly that.
+    const int fold_spin = p->n_items + p->n_norm_chunks + 1;
+    p->gfold = p->gfold && 2 * fold_spin <= n_cu_dev;
     if (const char* f = std::getenv("MCC_GFOLD")) p->gfold = p->gfold && std::atoi(f) != 0;
+    if (const char* f = std::getenv("MCC_FOLD_CONSUMERS_FIRST")) p->fold_first = p->gfold && std::atoi(f) != 0;
     if (p->gfold) {
         // the final workgroup's LDS (k_schur's one-level layout) within k_group's
         const size_t fs = mcc::schur_lds_bytes(p->m, 1, 1, 1, p->n_items + p->n_norm_chunks, p->nblk);
@@ -1116,9 +1183,11 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         // (config5's 500-view shard: the trailing items started 1.5 us after the last group ended).
         // Measured, not the default: config4 26.55 vs 26.41 us per step, config5's shard 29.3 vs 29.5
         // (interleaved, gpurun_out/r05u) -- the last group's slots, not the items' start, set the tail.
+        // With fold_dyn a finished group spins on slots of groups that may not have started, so the
+        // whole grid must be resident at once: the groups and the spare within one workgroup per CU.
         const char* fd = std::getenv("MCC_FOLD_DYN");
         p->fold_dyn = fd && std::atoi(fd) != 0 && p->n_pgroups >= 2 * (p->n_items + p->n_norm_chunks + 1) &&
-                      p->prism != 2;
+                      p->prism != 2 && p->n_pgroups + 1 <= n_cu_dev;
         if (p->fold_dyn) {
             HIPC(p->fold_ticket.alloc(1));
             HIPC(hipMemset(p->fold_ticket.p, 0, sizeof(int)));
@@ -1175,6 +1244,7 @@ void mcc_destroy(mcc_problem* p) {
     p->xsave.release(); p->ysave.release(); p->zpsave.release();
     for (auto e : p->ev_lin) (void)hipEventDestroy(e);
     for (auto e : p->ev_step) (void)hipEventDestroy(e);
+    for (auto e : p->ev_opt) if (e) (void)hipEventDestroy(e);
     for (auto e : p->ev_x) (void)hipEventDestroy(e);
     for (auto e : p->ev_marks) (void)hipEventDestroy(e);
     for (auto e : p->ev_win) if (e) (void)hipEventDestroy(e);
@@ -1198,6 +1268,7 @@ void mcc_destroy(mcc_problem* p) {
     p->pgrp_ptr.release(); p->pgrp_edge.release(); p->edge_lphoto.release(); p->gpair_ptr.release(); p->gcon_ptr.release(); p->gcon.release();
     p->state.release();
     if (p->h_state) (void)hipHostFree(p->h_state);
+    if (p->h_x) (void)hipHostFree(p->h_x);
     if (drained) stream_pool().give(p->device, p->stream);   // a stream that faulted is not reused
     else if (p->stream) (void)hipStreamDestroy(p->stream);
     if (side_drained) stream_pool().give(p->device, p->side, true);
@@ -1253,23 +1324,68 @@ int mcc_optimize(mcc_problem* p, int crit_type, int max_count, double eps, float
                  double* last_change) {
     if (!p || !x_inout) return fail(MCC_EINVAL, "null argument");
     if (crit_type < 1 || crit_type > 3) return fail(MCC_EINVAL, "crit_type must be 1, 2 or 3");
-    int rc = mcc_set_params(p, x_inout, p->P);
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    HIPCHK(hipSetDevice(p->device));
+    int rc = begin_optimize(p, x_inout, crit_type, max_count, eps);
     if (rc) return rc;
-    if ((rc = set_state(p, 1, crit_type, max_count, eps))) return rc;
+    if (!p->ev_opt[0]) {
+        HIPCHK(hipEventCreate(&p->ev_opt[0]));
+        HIPCHK(hipEventCreate(&p->ev_opt[1]));
+    }
+    const auto t1 = clk::now();
+    HIPCHK(hipEventRecord(p->ev_opt[0], p->stream));
     const long long cap = crit_type == MCC_CRIT_EPS ? 1000000LL : (long long)max_count + 1;
     long long launched = 0;
+    int polls = 0;
     while (true) {
         const int chunk = mcc_problem::kGraphSteps;
         if ((rc = launch_update_steps(p, chunk))) return rc;
+        HIPCHK(hipEventRecord(p->ev_opt[1], p->stream));
         launched += chunk;
+        ++polls;
         if ((rc = read_state(p))) return rc;
         if ((rc = check_state_error(p))) return rc;
         if (p->h_state->done) break;
         if (launched > cap + chunk) return fail(MCC_EINVAL, "optimize did not terminate");
     }
+    const auto t2 = clk::now();
     if (iters) *iters = p->h_state->iter;
     if (last_change) *last_change = p->h_state->change;
-    return mcc_get_params(p, x_inout, p->P);
+    p->opt_iters = p->h_state->iter;
+    // the finish: the pending photo update flushed (the state was read by the last poll), the
+    // parameters out -- one synchronisation
+    if (p->h_state->pending) {
+        if ((rc = enqueue_backsub(p, 1))) return rc;
+        p->h_state->pending = 0;
+        HIPCHK(hipMemsetAsync(&p->state.p->pending, 0, sizeof(int), p->stream));
+    }
+    HIPCHK(hipMemcpyAsync(p->h_x, p->x.p, sizeof(float) * p->P, hipMemcpyDeviceToHost, p->stream));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    std::memcpy(x_inout, p->h_x, sizeof(float) * p->P);
+    const auto t3 = clk::now();
+    float dev = 0.f;
+    if (hipEventElapsedTime(&dev, p->ev_opt[0], p->ev_opt[1]) != hipSuccess) dev = -1.f;
+    p->opt_dev_ms = dev;
+    p->opt_host_ms[0] = ms(t0, t1);
+    p->opt_host_ms[1] = ms(t1, t2);
+    p->opt_host_ms[2] = ms(t2, t3);
+    p->opt_host_ms[3] = ms(t0, t3);
+    p->opt_launched = (int)launched;
+    p->opt_polls = polls;
+    return rc;
+}
+
+int mcc_optimize_profile(mcc_problem* p, double* host_ms, double* device_ms, int* launched, int* iters,
+                         int* polls) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    if (host_ms) std::memcpy(host_ms, p->opt_host_ms, sizeof(p->opt_host_ms));
+    if (device_ms) *device_ms = p->opt_dev_ms;
+    if (launched) *launched = p->opt_launched;
+    if (iters) *iters = p->opt_iters;
+    if (polls) *polls = p->opt_polls;
+    return MCC_OK;
 }
 
 int mcc_step(mcc_problem* p, int n) {
@@ -1402,6 +1518,22 @@ int mcc_solve_stats(mcc_problem* p, long long* out) {
     HIPCHK(hipStreamSynchronize(p->stream));
     if (p->side) HIPCHK(hipStreamSynchronize(p->side));
     HIPCHK(hipMemcpy(out, p->warm_stats.p, 5 * sizeof(long long), hipMemcpyDeviceToHost));
+    return MCC_OK;
+}
+
+int mcc_debug_delays(mcc_problem* p, double spare_delay_us, double warm_delay_us, double warm_timeout_ms) {
+    if (!p) return fail(MCC_EINVAL, "null problem");
+    HIPCHK(hipSetDevice(p->device));
+    HIPCHK(hipStreamSynchronize(p->stream));
+    if (p->side) HIPCHK(hipStreamSynchronize(p->side));
+    if (spare_delay_us >= 0.0) p->spare_delay_ticks = (long long)(spare_delay_us * 1e2);
+    if (warm_delay_us >= 0.0) p->warm_delay_ticks = (long long)(warm_delay_us * 1e2);
+    if (warm_timeout_ms >= 0.0) {
+        const long long w = (long long)(std::max(1.0, warm_timeout_ms) * 1e5);
+        p->warm_idle_ticks += w - p->warm_wait_ticks;   // (the idle exit keeps its margin over the bound)
+        p->warm_wait_ticks = w;
+    }
+    drop_graphs(p);   // (the delays and the bound are kernel arguments)
     return MCC_OK;
 }
 

@@ -295,8 +295,13 @@ __device__ __forceinline__ void group_chain(GroupChain& CH, const double* Gbe, i
 // handed-off word is its own flag (kFoldEmpty until the producer's 8-byte sc1 store lands; 8-byte
 // aligned halves of a store are single-copy atomic), each consumer polls the words it needs with sc1
 // loads and writes kFoldEmpty back once it has read them, so the words are empty again before the next
-// launch's producers (after the kernel boundary).  A consumer waits only on workgroups with lower grid
-// indices, which are dispatched before it, so the grid needs no co-residency.  The sums are k_schur's,
+// launch's producers (after the kernel boundary).  Progress needs no dispatch order and no
+// co-residency of the whole grid: producers (groups, spare) never wait, and mcc_create takes the fold
+// only while the spinning consumers fill at most half of the CUs (one k_group workgroup fits per CU),
+// so in any dispatch order a slot stays free for some producer, which runs to its end
+// (MCC_FOLD_CONSUMERS_FIRST=1 puts the consumers at the lowest grid indices to test exactly that).
+// fold_dyn is the exception: a finished group spins on groups that may not have started, so it needs
+// the whole grid resident (mcc_create: groups + spare <= CUs).  The sums are k_schur's,
 // in its order (kSub sub-chunks per item entry, chunks in photo order, items in item order), so the
 // bits are the k_group -> k_schur step's.  Where k_schur's boundary and item phase followed the last
 // group (~4 us at config4), the items here have summed most slots by then.
@@ -314,6 +319,10 @@ __device__ __forceinline__ bool fold_timed_out(const LinArgs& a, long long t0) {
 // order), each thread loading all of its slots in one batch and adding the valid prefix in order; the
 // item's 48-entry partial -> fsa.item_out (sc1)
 constexpr int kFoldSlots = 13;   // slots per thread: items of <= 64 slots (mcc_create) over kSub sub-chunks
+// (The batch is re-issued back to back while slots are missing.  Round 6 measured the polls' cost: a
+// sleeping single-slot pre-wait for items dispatched while the groups run left the step's memory-side
+// traffic at 12.94 MB against 13.04 (config4), and its extra round trip for items that start late cost
+// +0.5 us per step)
 __device__ __forceinline__ void fold_item(const LinArgs& la, int item) {
     const SchurArgs& a = la.fsa;
     const int tid = threadIdx.x;
@@ -491,7 +500,8 @@ __device__ __forceinline__ void fold_final_u(const LinArgs& la) {
     for (int k = a.n_items; k < np; ++k) err_now |= itm[48 * k + 2] != 0.0 ? kErrPhotoNotPD : 0;
     __syncthreads();
     SSTAMP(srow, 8, 0);   // the partials landed in LDS
-    schur_finish(a, np, iter, cn0, cn1, err_now, useiv && s_status > 0, srow);
+    // (the inverse only with this launch's tag: fold_final_direct)
+    schur_finish(a, np, iter, cn0, cn1, err_now, useiv && s_status == (double)(iter + 1), srow);
 }
 // The final workgroup with the sums formed where the words land (LinArgs::fold_direct: 512 threads,
 // <= 8 items per camera-pair block, <= 4 norm chunks -- config4): thread t < 48 nblk owns entry t of
@@ -606,7 +616,11 @@ __device__ __forceinline__ void fold_final_direct(const LinArgs& la) {
         return;
     }
     SSTAMP(srow, 8, 0);   // every word landed
-    const bool ivok = useiv && s_stt > 0.0;
+    // the inverse only with this launch's tag, +(iteration + 1) (the spare's status is +-(iteration + 1));
+    // a status another launch left would read as landed, and its inverse is not this system's: the
+    // step then eliminates directly (set_state empties every word after a failed launch, so this is a
+    // guard, not a path)
+    const bool ivok = useiv && s_stt == (double)(iter + 1);
     if (kind == 1 && cnt > 0) {
         double v = 0.0;
 #pragma unroll
@@ -706,10 +720,10 @@ __device__ __forceinline__ void fold_final(const LinArgs& la) {
 #endif
 // The group's work (phases 0, A, B above); false when the loop has stopped (nothing done).
 template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
-__device__ __forceinline__ bool group_body(const LinArgs& a) {
+__device__ __forceinline__ bool group_body(const LinArgs& a, const int grp) {
     constexpr int NT = kGroupRound * L, EPW = 64 / L;   // threads; edges per wave
     State* st = a.state;
-    const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // ---- round trip 1: the state and the group's ranges (the stop test after the loads are issued)
     const int done = st->done, pending = st->pending;
     const double alpha_prev = st->alpha;   // step factor of the pending update
@@ -1256,7 +1270,14 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
     constexpr int NT = kGroupRound * L;
     static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
-    const int grp = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
+    int grp = blockIdx.x;
+#ifndef MCC_NO_FOLD_FIRST   // (A/B builds: the layout switch's cost)
+    if (a.fold_first) {   // (test layout: the trailing workgroups first, then the groups)
+        const int nlead = (int)gridDim.x - a.n_pgroups;
+        grp = grp < nlead ? a.n_pgroups + grp : grp - nlead;
+    }
+#endif
     if (a.ssinv && grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
         extern __shared__ __attribute__((aligned(16))) double smem_spare[];
         small_inverse(a, smem_spare, false);
@@ -1272,7 +1293,7 @@ __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_gro
         if (st->done) return;
         task = grp - a.n_pgroups - (a.ssinv ? 1 : 0);
     } else {
-        if (!group_body<MODEL, RATIONAL, PRISM, BACK, L>(a) || PRISM == 2 || !a.fold_dyn) return;
+        if (!group_body<MODEL, RATIONAL, PRISM, BACK, L>(a, grp) || PRISM == 2 || !a.fold_dyn) return;
         __shared__ int s_task;
         __syncthreads();   // the group's LDS is free
         if (tid == 0) {

@@ -152,6 +152,10 @@ struct LinArgs {
     int fault_photo;         // test (MCC_FAULT_PHOTO): this local photo's 6 x 6 block is reported not
                              // positive definite (its factor stays finite); -1 off
     // m <= 30 warm solve: k_group's spare workgroup inverts the previous step's packed system
+    int fold_first;          // test layout (MCC_FOLD_CONSUMERS_FIRST=1): the spare and the folded reduction's
+                             // workgroups take the LOWEST grid indices, the groups the rest -- the
+                             // progress invariant must not rest on dispatch order (mcc_create); (placed
+                             // in fault_photo's padding: a shifted LinArgs tail cost k_group SGPR spills)
     double* ssinv;           // [2][m x m] by iteration parity (null: off)
     int* ssinv_ok;           // [2] the iteration + 1 whose spare workgroup formed the buffer (0: none)
     // the fused step's spare: its wait bound at the final arriver (s_memrealtime ticks; past it the

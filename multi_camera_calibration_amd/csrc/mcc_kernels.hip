@@ -978,7 +978,12 @@ __device__ __forceinline__ bool spare_wait(const LinArgs& a, unsigned ack, unsig
     return false;
 }
 // after a barrier behind every thread's spare_wait: the spare never acknowledged -> fail the step
-// (MCC_ETIMEOUT), stop the loop; nothing of the step was written
+// (MCC_ETIMEOUT), stop the loop.  Neither the state nor the solve is written.  The packed system may be:
+// each thread writes its entries as soon as its own spare_wait returns, so when the acknowledgement
+// lands at the bound some threads have written theirs and the others gave up.  That copy is read only
+// as the next update launch's spare input (a pending update); a new optimisation (mcc_set_params)
+// starts with none, so a failed step's packed system is never inverted
+// (tests/test_warm_solve.py::test_fused_spare_timeout_fails_the_step runs one on the same handle)
 __device__ __forceinline__ bool spare_failed(State* st, int ack_to) {
     if (!ack_to) return false;
     if (threadIdx.x == 0) {
@@ -1447,9 +1452,9 @@ __global__ __launch_bounds__(256, 2) void k_linearize(LinArgs a) {
     __shared__ double nrm2[2];
     const int iter0 = P.iter0;   // read before S overwrites the photo record
     const double cnG = P.cn[0], cnX = P.cn[1];
-    // the spare's acknowledgement of this launch (small_inverse): no thread writes the packed system or
+    // the spare's acknowledgement of this launch (small_inverse): no thread writes its packed entries or
     // the state before it has seen it; a thread that gave up (spare_wait's bound) sets ack_to, and the
-    // step then fails after the next barrier instead of solving
+    // step then fails after the next barrier instead of solving (spare_failed: what a failed step leaves)
 #ifdef MCC_NO_SPARE_ACK   // (A/B builds only: the round-4 race, for pricing the acknowledgement)
     const bool spare = false;
 #else

@@ -23,7 +23,7 @@ from multi_camera_calibration_amd import api, rig
 from oracle import oracle_py as O
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from ulp import f32_ulp_diff, state_resolution_diff  # noqa: E402
+from ulp import f32_ulp_diff, report, state_resolution_diff  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -60,6 +60,8 @@ def test_full_size_optimize(full):
     assert abs(m - m_ref) <= 1e-6, (name, m, m_ref)
     ulp = f32_ulp_diff(x, x_ref)
     res = state_resolution_diff(x, x_ref)
+    report(f"{name}_x1", x, x_ref, world=1, iters_gpu=int(it), iters_oracle=int(it_ref), mean_gpu=float(m),
+           mean_oracle=float(m_ref), mean_abs_diff_px=abs(float(m) - float(m_ref)))
     print(f"{name}: {int((ulp > 0).sum())} of {ulp.size} parameters differ, max {int(ulp.max())} ulp, "
           f"{res:.2f} x the state's float32 resolution")
     assert res <= 2.0, (name, res, int(ulp.max()), int((ulp > 0).sum()))

@@ -29,7 +29,7 @@ from oracle import oracle_py as O
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import peer_worker  # noqa: E402
-from ulp import f32_ulp_diff, state_resolution_diff  # noqa: E402
+from ulp import f32_ulp_diff, report, state_resolution_diff  # noqa: E402
 
 
 def test_peer_abi_declared():
@@ -125,6 +125,9 @@ def test_peer_ranks_one_device(case, world, tmp_path):
     _, mean = o.project_error(x)
     assert abs(mean - m_ref) <= 1e-6, (case, world, mean, m_ref)
     ulp = f32_ulp_diff(x, x_ref)
+    report(f"{case}_x{world}", x, x_ref, world=world, iters_gpu=int(outs[0]["it"]), iters_oracle=int(it_ref),
+           mean_gpu=float(mean), mean_oracle=float(m_ref), mean_abs_diff_px=abs(float(mean) - float(m_ref)),
+           transport="peer (ranks as processes on one device)")
     if case.endswith("_full"):
         res = state_resolution_diff(x, x_ref)
         print(f"{case} x{world}: {int((ulp > 0).sum())} of {ulp.size} parameters differ, {res:.2f} x resolution")

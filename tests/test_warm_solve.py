@@ -173,14 +173,25 @@ def test_helper_refinement_is_bitwise_k_solves(name):
     assert st1["warm"] > 0
 
 
+def _recovers_on_the_same_handle(ba, p, fresh_env):
+    """after a failed optimisation: the delays off, the same handle optimises again and gives bitwise
+    a fresh problem's result (nothing the failed launch left behind is read)"""
+    ba.debug_delays(spare_delay_us=0, warm_delay_us=0, warm_timeout_ms=10000)
+    x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+    xf, mf, itf, _ = run(p, fresh_env)
+    assert it == itf and m == mf, (it, itf, m, mf)
+    assert np.array_equal(x, xf)
+
+
 def test_helper_timeout_fails_the_step():
     """A helper slower than MCC_WARM_TIMEOUT_MS: the step fails with MCC_ETIMEOUT (-6) instead of
-    switching algorithms, and the problem recovers on the next optimisation."""
+    switching algorithms, and the problem recovers on the next optimisation of the same handle."""
     p = CASES["config3_small"]()
     ba = make(p, {"MCC_WARM_DELAY_US": "30000", "MCC_WARM_TIMEOUT_MS": "3"})
     try:
         with pytest.raises(api.MccError, match=r"\(-6\)"):
             ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+        _recovers_on_the_same_handle(ba, p, {})
     finally:
         ba.close()
 
@@ -275,6 +286,7 @@ def test_fused_spare_timeout_fails_the_step():
     try:
         with pytest.raises(api.MccError, match=r"\(-6\)"):
             ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+        _recovers_on_the_same_handle(ba, p, {})
     finally:
         ba.close()
     x, m, it, _ = run(p, {})
@@ -317,11 +329,15 @@ def test_folded_group_step_is_bitwise_the_two_kernel_step(views):
     workgroup held back 300 us (its status word is what the final workgroup waits for before it writes
     the packed system and the state) the bits do not move.  1 000 views is config4 itself (250 groups on
     256 CUs: the items start only when groups exit).  MCC_FOLD_DYN=1 (the groups take the reduction's
-    tasks by ticket as they finish, no trailing workgroups) gives the same bits.  src/multicalib.cpp:462-514."""
+    tasks by ticket as they finish, no trailing workgroups) gives the same bits.  So does the grid laid out
+    with the consumers (spare, items, norm chunks, final) at the LOWEST indices
+    (MCC_FOLD_CONSUMERS_FIRST=1): progress does not rest on the dispatcher starting the groups first,
+    only on the consumers leaving CUs for the producers (mcc_create).  src/multicalib.cpp:462-514."""
     p = rig.make_config("config4", n_views=views)
     runs = []
     for env in ({"MCC_GFOLD": "0"}, {}, {"MCC_SPARE_DELAY_US": "300"}, {"MCC_FOLD_DYN": "1"},
-                {"MCC_FOLD_DYN": "1", "MCC_SPARE_DELAY_US": "300"}):
+                {"MCC_FOLD_DYN": "1", "MCC_SPARE_DELAY_US": "300"}, {"MCC_FOLD_CONSUMERS_FIRST": "1"},
+                {"MCC_FOLD_CONSUMERS_FIRST": "1", "MCC_SPARE_DELAY_US": "300"}):
         ba = make(p, dict(env, MCC_FUSED="0", MCC_SOLVE_STATS="1"))
         try:
             assert ba.step_kernels() == "k_group"
@@ -344,3 +360,22 @@ def test_folded_group_step_is_bitwise_the_two_kernel_step(views):
         for k in ("warm", "corrections", "fallbacks", "direct"):
             assert st[k] == st0[k], (st0, st)
     assert st0["warm"] > 0
+
+
+def test_folded_timeout_then_same_handle_is_a_fresh_run():
+    """The folded k_group step (config4 rig, 200 views) with its spare held back 30 ms against a 3 ms
+    poll bound: the final workgroup gives up, the step fails with MCC_ETIMEOUT (-6), and the late spare
+    still writes its inverse and status, the final's item partials stay unread.  The next optimisation
+    on the SAME handle (delays off) starts with every hand-off word empty again (set_state after an
+    error) and is bitwise a fresh problem's run; the consumers-first layout recovers the same way."""
+    p = rig.make_config("config4", n_views=200)
+    for extra in ({}, {"MCC_FOLD_CONSUMERS_FIRST": "1"}):
+        env = dict(extra, MCC_FUSED="0")
+        ba = make(p, dict(env, MCC_SPARE_DELAY_US="30000", MCC_WARM_TIMEOUT_MS="3"))
+        try:
+            assert ba.folded()
+            with pytest.raises(api.MccError, match=r"\(-6\)"):
+                ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+            _recovers_on_the_same_handle(ba, p, env)
+        finally:
+            ba.close()

@@ -26,3 +26,23 @@ def state_resolution_diff(a, b):
         res = float(np.spacing(np.float32(np.abs(b[:, cols]).max())))
         out = max(out, float(d[:, cols].max()) / res)
     return out
+
+
+def report(case, x, x_ref, **extra):
+    """MCC_PARITY_REPORT=<dir>: one JSON record per final-iterate comparison (tools/ulp_report.py --final
+    collects them): how many float32 parameters differ from the oracle's, by how many ulps, and the
+    state-resolution distance the full-size bar uses."""
+    import json
+    import os
+    d = os.environ.get("MCC_PARITY_REPORT")
+    if not d:
+        return
+    ulp = f32_ulp_diff(x, x_ref)
+    hist = {"0": int((ulp == 0).sum()), "1": int((ulp == 1).sum()), "2-4": int(((ulp >= 2) & (ulp <= 4)).sum()),
+            "5-16": int(((ulp >= 5) & (ulp <= 16)).sum()), "17-256": int(((ulp >= 17) & (ulp <= 256)).sum()),
+            ">256": int((ulp > 256).sum())}
+    rec = dict(case=case, params=int(ulp.size), differ=int((ulp > 0).sum()), max_ulp=int(ulp.max()),
+               ulp_histogram=hist, state_resolution_diff=float(state_resolution_diff(x, x_ref)), **extra)
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, f"{case}.json"), "w") as f:
+        json.dump(rec, f, indent=1)

@@ -24,7 +24,29 @@ from oracle import oracle_py as O  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("configs", nargs="*", default=["config1", "config2", "config3", "config4", "config5"])
 ap.add_argument("--out", default=None)
+ap.add_argument("--final", default=None, metavar="DIR",
+                help="collect the final-iterate records the GPU parity tests wrote with MCC_PARITY_REPORT=DIR "
+                     "(tests/test_full_size.py::test_full_size_optimize, tests/test_peer_transport.py::"
+                     "test_peer_ranks_one_device) into --out instead")
 args = ap.parse_args()
+if args.final:
+    recs = {}
+    for fn in sorted(os.listdir(args.final)):
+        if fn.endswith(".json"):
+            r = json.load(open(os.path.join(args.final, fn)))
+            recs[r["case"]] = r
+            print(r["case"], {k: r[k] for k in ("differ", "params", "max_ulp", "state_resolution_diff",
+                                                  "iters_gpu", "iters_oracle", "mean_abs_diff_px")}, flush=True)
+    res = {"what": "final optimizeExtrinsics iterates (COUNT+EPS, 200, eps 1e-7, from x0) of the GPU path against the "
+                   "oracle's on the whole problem: float32 parameters that differ, the largest difference in ulps, "
+                   "an ulp histogram, and state_resolution_diff (tests/ulp.py: the difference in units of the "
+                   "float32 spacing of the largest rotation / translation the state holds; the full-size bar is "
+                   "<= 2); *_x1 from tests/test_full_size.py, *_xN from tests/test_peer_transport.py (N ranks as "
+                   "processes on one device, peer transport)",
+           "cases": recs}
+    if args.out:
+        json.dump(res, open(args.out, "w"), indent=1)
+    sys.exit(0)
 rows = {}
 for cfg in args.configs:
     t0 = time.time()
