@@ -287,6 +287,16 @@ def optimize_line(name: str, reps: int = 20, device: int = 0):
             wall = (time.perf_counter() - t0) * 1e3
             rows.append(dict(ba.optimize_profile(), wall_ms=wall))
         path = ba.step_kernels() + (" (folded)" if ba.folded() else "")
+        # the itemisation: device ms of the same call under COUNT with max_count = k (k updates, the
+        # stop-test launch, then no-op launches to the end of the 8-step graph), median of 5 calls each;
+        # cost(k) - cost(k - 1) is the k-th update step in place of a no-op launch
+        by_count = []
+        for k in range(0, it + 1):
+            dv = []
+            for _ in range(5):
+                ba.optimize_extrinsics(p.x0, crit_type=1, max_count=k)
+                dv.append(ba.optimize_profile()["device_ms"])
+            by_count.append(float(np.median(dv)))
     finally:
         ba.close()
     old = os.environ.get("MCC_SOLVE_STATS")
@@ -314,7 +324,12 @@ def optimize_line(name: str, reps: int = 20, device: int = 0):
             "steps_launched": rows[-1]["steps_launched"], "stop_polls": rows[-1]["stop_polls"],
             "first_call": {"wall_ms": first_wall, "host_ms": first["host_call_ms"], "device_ms": first["device_ms"],
                            "note": "graph capture on first use"},
-            "solves_per_call": {k: s1[k] - s0[k] for k in ("warm", "corrections", "fallbacks", "direct", "waited")}}
+            "solves_per_call": {k: s1[k] - s0[k] for k in ("warm", "corrections", "fallbacks", "direct", "waited")},
+            "device_ms_by_count": {"max_count": list(range(0, it + 1)), "device_ms": by_count,
+                                   "marginal_ms": [by_count[k] - by_count[k - 1] for k in range(1, it + 1)],
+                                   "note": "COUNT criterion, max_count = k: k updates + the stop-test launch + no-op "
+                                           "launches to the end of the 8-step graph; marginal = an update step in "
+                                           "place of a no-op launch"}}
 
 
 def strong_line(name: str, rank: int, world: int, local_rank: int, same_device: bool, steps: int = 100):

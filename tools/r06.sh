@@ -26,7 +26,7 @@ for s in "$@"; do
       timeout -k 10 300 python bench.py --optimize-only > $OUT/opt.json 2> $OUT/opt.err || exit 12
       python3 -c "
 import json; d=json.load(open('$OUT/opt.json'))['optimize']
-for k,v in d.items(): print(k, v['iterations'], 'iters; wall', round(v['wall_ms_per_call'],3), 'ms; device', round(v['device_ms_per_call'],3), 'ms,', round(v['device_ms_per_iteration']*1e3,1), 'us/iter; host', {a: round(b,3) for a,b in v['host_ms'].items()}, v['solves_per_call'])
+for k,v in d.items(): print(k, v['iterations'], 'iters; wall', round(v['wall_ms_per_call'],3), 'ms; device', round(v['device_ms_per_call'],3), 'ms,', round(v['device_ms_per_iteration']*1e3,1), 'us/iter; host', {a: round(b,3) for a,b in v['host_ms'].items()}, v['solves_per_call'], 'by count', [round(x*1e3,1) for x in v['device_ms_by_count']['device_ms']])
 " ;;
     prof:*)
       bash tools/profile_round.sh $TAG ${s#prof:} > $OUT/prof_${s#prof:}.log 2>&1 || { tail -5 $OUT/prof_${s#prof:}.log; exit 13; }
