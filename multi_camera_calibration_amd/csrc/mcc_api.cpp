@@ -1162,7 +1162,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     const int fold_spin = p->n_items + p->n_norm_chunks + 1;
     p->gfold = p->gfold && 2 * fold_spin <= n_cu_dev;
     if (const char* f = std::getenv("MCC_GFOLD")) p->gfold = p->gfold && std::atoi(f) != 0;
-    if (const char* f = std::getenv("MCC_FOLD_CONSUMERS_FIRST")) p->fold_first = p->gfold && std::atoi(f) != 0;
+    if (const char* f = std::getenv("MCC_FOLD_CONSUMERS_FIRST"))   // (a test instantiation, omnidir rigs)
+        p->fold_first = p->gfold && p->model == MCC_MODEL_OMNI && std::atoi(f) != 0;
     if (p->gfold) {
         // the final workgroup's LDS (k_schur's one-level layout) within k_group's
         const size_t fs = mcc::schur_lds_bytes(p->m, 1, 1, 1, p->n_items + p->n_norm_chunks, p->nblk);

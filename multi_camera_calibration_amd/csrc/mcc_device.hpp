@@ -96,13 +96,54 @@ __device__ __forceinline__ void so3_jac_inv(const double w[3], double th, double
     so3_poly(w, -sign * 0.5, ci, J);
 }
 
-// cvRodrigues2 matrix -> vector (acos branch and the s < 1e-5 branches), returning the angle's
-// trig (th, s, c) for the inverse Jacobians.  The SVD re-orthonormalisation OpenCV applies
-// first changes an FP64 product of two rotations only at the 1e-16 level.
-__device__ __forceinline__ void rodrigues_m2v(const double* R, double* r, double& th_o, double& s_o, double& c_o) {
+// The oracle's restatement of the re-orthonormalisation cvRodrigues2 applies first (SVD, U V^T), as a
+// Newton iteration X <- (X + X^-T) / 2 in its operation order (oracle/mcc_oracle.c polar3).
+__device__ __forceinline__ void polar3_ora(double* R) {
 #pragma clang fp contract(off)
+    for (int it = 0; it < 40; ++it) {
+        const double d = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                         R[2] * (R[3] * R[7] - R[4] * R[6]);
+        if (!(fabs(d) > 1e-300)) break;
+        double cof[9];
+        cof[0] = R[4] * R[8] - R[5] * R[7];
+        cof[1] = -(R[3] * R[8] - R[5] * R[6]);
+        cof[2] = R[3] * R[7] - R[4] * R[6];
+        cof[3] = -(R[1] * R[8] - R[2] * R[7]);
+        cof[4] = R[0] * R[8] - R[2] * R[6];
+        cof[5] = -(R[0] * R[7] - R[1] * R[6]);
+        cof[6] = R[1] * R[5] - R[2] * R[4];
+        cof[7] = -(R[0] * R[5] - R[2] * R[3]);
+        cof[8] = R[0] * R[4] - R[1] * R[3];
+        double delta = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const double v = 0.5 * (R[k] + cof[k] / d);
+            const double df = fabs(v - R[k]);
+            if (df > delta) delta = df;
+            R[k] = v;
+        }
+        if (delta < 1e-15) break;
+    }
+}
+
+// cvRodrigues2 matrix -> vector (acos branch and the s < 1e-5 branches), returning the angle's
+// trig (th, s, c) for the inverse Jacobians.  The SVD re-orthonormalisation OpenCV applies first
+// changes an FP64 product of two rotations only at the 1e-16 level, and the vector by ~1e-16 / s:
+// it is skipped unless s < 1e-3 (theta near 0 or pi), where the vector's float32 rounding (and in
+// the s < 1e-5 branch near pi, which reads the axis from the diagonal, the pixel) follows it --
+// there the oracle's restatement runs first, as in the reference (tests/test_rodrigues_branch.py).
+__device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, double& th_o, double& s_o, double& c_o) {
+#pragma clang fp contract(off)
+    double R[9];   // (a register copy: a pointer switched between the input and a polar copy made a stack array)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) R[k] = Rin[k];
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    if (s < 1e-3) {
+        polar3_ora(R);
+        rx = R[7] - R[5]; ry = R[2] - R[6]; rz = R[3] - R[1];
+        s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    }
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
     double theta = acos(c);
@@ -126,6 +167,14 @@ __device__ __forceinline__ void rodrigues_m2v(const double* R, double* r, double
     }
     r[0] = rx; r[1] = ry; r[2] = rz;
 }
+
+// cvRodrigues2's derivative d om / d R in its s < 1e-5 branch near theta = pi (c <= 0) is ZERO (it
+// fills the 3 x 9 Jacobian only for c > 0), so compose_motion's d om3 / d om1 and d om3 / d om2 vanish
+// for a composed rotation within ~1e-5 rad of pi (DoubleSide rigs: a camera facing the board's back;
+// config5's rig has one such edge after its first update).  The closed-form inverse Jacobians below
+// would give the true derivative there; the reference gives 0, and so do we (rot_jzero).  (Near
+// theta = 0, c > 0, OpenCV's fixed 0.5 pattern equals the closed form to O(theta) < 1e-5.)
+__device__ __forceinline__ bool rot_jzero(double s, double c) { return s < 1e-5 && !(c > 0); }
 
 // Polar factor (U V^T) by Newton iteration, for float32 products of rotations (metric path).
 __device__ __forceinline__ void polar3(double* R) {
@@ -187,6 +236,10 @@ __device__ __forceinline__ void compose(const double* R1, const double* Jr1, con
     mat3_mul(Ji, Jr1, m.A1);
     so3_jac_inv(m.om, th, s, c, +1.0, Ji);   // Jl^-1(om3)
     mat3_mul(Ji, Jl2, m.A2);
+    if (rot_jzero(s, c)) {   // (cvRodrigues2's theta ~ pi branch)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) m.A1[k] = m.A2[k] = 0.0;
+    }
     const double qx[9] = {0, q[2], -q[1], -q[2], 0, q[0], q[1], -q[0], 0};   // -[q]x
     mat3_mul(qx, Jl2, m.B2);
 }

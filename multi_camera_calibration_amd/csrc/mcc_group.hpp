@@ -70,7 +70,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
             negskew_row(q, i, row);
         }
         const double* B = blk == 0 ? Jr1 : Jl2;
-        W[e] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+        W[e] = blk < 2 && rot_jzero(sn, cs) ? 0.0 : row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];   // (rot_jzero)
     }
     wave_sync_lds();
     if (!BACK || side != MCC_BACK) {
@@ -151,7 +151,7 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         } else {
             so3_poly_col(om, fa, fb, j, bc);   // column j of Jlf (registers: no private array)
         }
-        Wb[e] = row[0] * bc[0] + row[1] * bc[1] + row[2] * bc[2];
+        Wb[e] = blk < 2 && rot_jzero(snb, csb) ? 0.0 : row[0] * bc[0] + row[1] * bc[1] + row[2] * bc[2];
     }
     wave_sync_lds();
     double rf[3], Tf[3];
@@ -1265,19 +1265,21 @@ __device__ __forceinline__ bool group_body(const LinArgs& a, const int grp) {
     return true;
 }
 
-template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
+// FIRST (a test instantiation, omnidir only: LinArgs::fold_first): the trailing workgroups (spare,
+// items, norm chunks, final) take the lowest grid indices and the groups the rest.  A separate
+// instantiation: remapping the index in the product kernel cost its register allocation ~230 more
+// SGPR-spill reloads and config4 ~0.2-0.4 us per step.
+template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L, bool FIRST = false>
 __global__ __launch_bounds__(kGroupRound * L, MCC_GROUP_OCC * 16 / L) void k_group(LinArgs a) {
     constexpr int NT = kGroupRound * L;
     static_assert(L == 16 || L == 32, "k_group: 16 or 32 lanes per edge");
     State* st = a.state;
     const int tid = threadIdx.x;
     int grp = blockIdx.x;
-#ifndef MCC_NO_FOLD_FIRST   // (A/B builds: the layout switch's cost)
-    if (a.fold_first) {   // (test layout: the trailing workgroups first, then the groups)
+    if (FIRST) {   // (test layout: the trailing workgroups first, then the groups)
         const int nlead = (int)gridDim.x - a.n_pgroups;
         grp = grp < nlead ? a.n_pgroups + grp : grp - nlead;
     }
-#endif
     if (a.ssinv && grp == a.n_pgroups) {   // the spare workgroup: the previous system's inverse (m <= 30 warm solve)
         extern __shared__ __attribute__((aligned(16))) double smem_spare[];
         small_inverse(a, smem_spare, false);

@@ -466,7 +466,7 @@ __device__ __forceinline__ void edge_prologue_wave(const PhotoLds& P, const doub
             negskew_row(q, i, row);
         }
         const double* B = blk == 0 ? P.Jr1 : Jl2;
-        W[lane] = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+        W[lane] = blk < 2 && rot_jzero(sn, cs) ? 0.0 : row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
     }
     if (side != MCC_BACK) {
         wave_sync_lds();
@@ -544,7 +544,7 @@ __device__ __forceinline__ void edge_prologue_wave(const PhotoLds& P, const doub
         } else {
             so3_poly_col(om, fa, fb, j, col);
         }
-        const double v = row[0] * col[0] + row[1] * col[1] + row[2] * col[2];
+        const double v = blk < 2 && rot_jzero(snb, csb) ? 0.0 : row[0] * col[0] + row[1] * col[1] + row[2] * col[2];
         if (blk == 0) W[27 + e] = v;
         else Wb[(blk - 1) * 9 + e] = v;
     }
@@ -4501,9 +4501,13 @@ template <int MODEL, bool RATIONAL, int PRISM, bool BACK, int L>
 static hipError_t launch_group_t(const LinArgs& a, size_t shmem, hipStream_t s) {
     // + the spare workgroup of the m <= 30 warm solve (small_inverse)
     // (+ the folded reduction's item, norm-chunk and final workgroups)
-    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>),
-                       dim3(a.n_pgroups + (a.ssinv ? 1 : 0) + (a.fold && !a.fold_dyn ? a.fold_parts + 1 : 0)),
-                       dim3(kGroupRound * L), shmem, s, a);
+    const dim3 grid(a.n_pgroups + (a.ssinv ? 1 : 0) + (a.fold && !a.fold_dyn ? a.fold_parts + 1 : 0));
+    if (a.fold_first) {   // (test layout, omnidir only: mcc_create)
+        if (MODEL != MCC_MODEL_OMNI) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_group<MCC_MODEL_OMNI, false, false, false, L, true>), grid, dim3(kGroupRound * L), shmem, s, a);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((k_group<MODEL, RATIONAL, PRISM, BACK, L>), grid, dim3(kGroupRound * L), shmem, s, a);
     return hipGetLastError();
 }
 template <int L>
@@ -4538,7 +4542,9 @@ static hipError_t set_group_attrs(size_t group_shmem) {
                          SETG(0, true, false, true), SETG(0, false, true, true), SETG(0, false, false, true),
                          SETG(0, true, true, false), SETG(0, true, false, false), SETG(0, false, true, false),
                          SETG(0, false, false, false), SETG(2, true, 2, true), SETG(0, true, 2, true),
-                         SETG(0, true, 2, false)})
+                         SETG(0, true, 2, false),
+                         hipFuncSetAttribute((const void*)&k_group<1, false, false, false, L, true>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_shmem)})
         if (e != hipSuccess) err = e;
 #undef SETG
     return err;

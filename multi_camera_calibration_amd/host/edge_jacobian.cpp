@@ -15,6 +15,7 @@
 // except at rare FP64 rounding ties of a transcendental.  The derivatives are the closed-form SO(3)
 // chain the device uses (d(R X)/dr = -[R X]x Jl(r); compose_motion's partials in composeMotion),
 // the same derivatives OpenCV's 3x9 Rodrigues / matMulDeriv chains evaluate.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -73,10 +74,41 @@ void rot_of(const double r[3], double R[9]) {
     for (int k = 0; k < 9; ++k) R[k] = c * (k % 4 == 0 ? 1.0 : 0.0) + c1 * rrt[k] + s * rx[k];
 }
 
-// cvRodrigues2 matrix -> vector (the acos branch and the s < 1e-5 branches near 0 and pi)
-void log_of(const double* R, double r[3]) {
+// the SVD re-orthonormalisation cvRodrigues2 applies first, as the oracle restates it (Newton
+// iteration X <- (X + X^-T) / 2, oracle/mcc_oracle.c polar3; the device's polar3_ora)
+void polar_of(const double* Rin, double* R) {
+    std::memcpy(R, Rin, 9 * sizeof(double));
+    for (int it = 0; it < 40; ++it) {
+        const double d = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                         R[2] * (R[3] * R[7] - R[4] * R[6]);
+        if (!(std::fabs(d) > 1e-300)) break;
+        const double cof[9] = {R[4] * R[8] - R[5] * R[7], -(R[3] * R[8] - R[5] * R[6]), R[3] * R[7] - R[4] * R[6],
+                               -(R[1] * R[8] - R[2] * R[7]), R[0] * R[8] - R[2] * R[6], -(R[0] * R[7] - R[1] * R[6]),
+                               R[1] * R[5] - R[2] * R[4], -(R[0] * R[5] - R[2] * R[3]), R[0] * R[4] - R[1] * R[3]};
+        double delta = 0;
+        for (int k = 0; k < 9; ++k) {
+            const double v = 0.5 * (R[k] + cof[k] / d);
+            delta = std::max(delta, std::fabs(v - R[k]));
+            R[k] = v;
+        }
+        if (delta < 1e-15) break;
+    }
+}
+
+// cvRodrigues2 matrix -> vector (the acos branch and the s < 1e-5 branches near 0 and pi); the
+// re-orthonormalisation only where the vector's float32 rounding follows it, s < 1e-3 (the device's
+// rodrigues_m2v)
+void log_of(const double* Rin, double r[3]) {
+    const double* R = Rin;
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
-    const double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double Rp[9];
+    if (s < 1e-3) {
+        polar_of(Rin, Rp);
+        R = Rp;
+        rx = R[7] - R[5]; ry = R[2] - R[6]; rz = R[3] - R[1];
+        s = std::sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    }
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
     double theta = std::acos(c);
@@ -234,6 +266,16 @@ void composeMotion(const double om1[3], const double T1[3], const double om2[3],
     mat3(Ji, Jr1, d[0]);                                   // dom3/dom1 = Jr(om3)^-1 Jr(om1)
     so3_jac(om3, +1.0, true, Ji);
     mat3(Ji, Jl2, d[2]);                                   // dom3/dom2 = Jl(om3)^-1 Jl(om2)
+    {
+        // cvRodrigues2's s < 1e-5 branch near theta = pi: d om / d R is zero there, so are both
+        // partials (mcc_device.hpp rot_jzero)
+        const double sx = R3[7] - R3[5], sy = R3[2] - R3[6], sz = R3[3] - R3[1];
+        const double s = std::sqrt((sx * sx + sy * sy + sz * sz) * 0.25);
+        double c = (R3[0] + R3[4] + R3[8] - 1) * 0.5;
+        c = c > 1. ? 1. : c < -1. ? -1. : c;
+        if (s < 1e-5 && !(c > 0))
+            for (int k = 0; k < 9; ++k) d[0][k] = d[2][k] = 0.0;
+    }
     const double qx[9] = {0, q[2], -q[1], -q[2], 0, q[0], q[1], -q[0], 0};   // -[R2 T1]x
     mat3(qx, Jl2, d[6]);                                   // dT3/dom2
     std::memcpy(d[5], R2, sizeof(R2));                     // dT3/dT1

@@ -1,0 +1,137 @@
+"""cvRodrigues2's theta ~ pi branch in compose_motion's derivatives (src/multicalib.cpp:1008-1056).
+
+OpenCV's matrix -> vector Rodrigues (cvRodrigues2, calib3d) takes a special branch when
+s = |sin theta| < 1e-5: near theta = pi (c <= 0) it reads the axis from the diagonal and leaves its
+3 x 9 Jacobian d om / d R at ZERO.  compose_motion chains that Jacobian, so for a composed rotation
+within ~1e-5 rad of pi the reference's d om3 / d om1 and d om3 / d om2 vanish, and the edge's
+rotation columns drop out of J.  The closed-form SO(3) chain (mcc_device.hpp) gives the true
+derivative there; the reference's semantics are kept by rot_jzero.  It happens on real rigs: a
+DoubleSide camera that faces the board's back composes with the photo to a rotation near pi
+(config5's synthetic rig has one such edge after its first update, s = 6.8e-7; before the fix its
+JTE differed from the oracle's by 3e-4 relative there and the final iterate by 4 283 parameters).
+
+  * CPU: the oracle's compose_motion (the OpenCV chain) has zero partials in the branch and the
+    closed form's elsewhere; the host per-edge Jacobian (libmcc_host.so) matches the oracle on an edge
+    moved into the branch;
+  * GPU: every step path (fused, k_group, three-kernel) matches the oracle's JTE and solved step on a
+    DoubleSide rig with one photo moved so that an edge lands in the branch.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from multi_camera_calibration_amd import api, rig
+from oracle import oracle_py as O
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import npmodel as N  # noqa: E402
+
+
+def _axis_angle(R):
+    w = N.log_so3(R)
+    th = np.linalg.norm(w)
+    return w / th, th
+
+
+def _rot(axis, th):
+    return N.rodrigues(np.asarray(axis, np.float64) * th)
+
+
+def test_oracle_compose_zero_partials_near_pi():
+    om2 = np.array([0.3, -0.2, 0.9])
+    R2 = N.rodrigues(om2)
+    axis = np.array([0.2, 0.96, 0.19]); axis /= np.linalg.norm(axis)
+    for dth, zero in ((2e-6, True), (3e-4, False)):
+        R3 = _rot(axis, np.pi - dth)
+        om1 = N.log_so3(R2.T @ R3)          # compose(photo om1, camera om2) = R2 R1 = R3
+        om3, _, d = O.compose_motion(om1, np.zeros(3), om2, np.zeros(3))
+        assert abs(np.linalg.norm(om3) - (np.pi - dth)) < 1e-8
+        if zero:
+            assert np.abs(d[0]).max() == 0.0 and np.abs(d[2]).max() == 0.0, d[0]
+        else:
+            assert np.abs(d[0]).max() > 0.1 and np.abs(d[2]).max() > 0.1
+
+
+def _branch_problem(model, n_views=12):
+    """A DoubleSide (or MyMulti BACK) rig with photo 0 rotated so that its first edge's composed rotation
+    R_cam R_photo is pi about its current axis (float32 state: |sin theta| ~ 1e-7 < 1e-5)."""
+    if model == "doubleside":
+        p = rig.make_config("config5", n_views=n_views)
+    else:
+        p = rig.make_config("config5", n_views=n_views, model=rig.PINHOLE, double_sided=True)
+    x = np.array(p.x0, np.float32)
+    best = None
+    for e in range(p.n_edges):   # the edge whose composition is nearest pi
+        c, v = int(p.edge_cam[e]), int(p.edge_photo[e])
+        col = p.photo_col(v)
+        omp = x[col:col + 3].astype(np.float64)
+        if p.model == rig.DOUBLESIDE:
+            Rc = np.asarray(p.cam_pose, np.float64).reshape(-1, 4, 4)[c][:3, :3]
+        elif c == 0:
+            Rc = np.eye(3)
+        else:
+            Rc = N.rodrigues(x[6 * (c - 1):6 * (c - 1) + 3].astype(np.float64))
+        R3 = Rc @ N.rodrigues(omp)
+        ax, th = _axis_angle(R3)
+        if best is None or th > best[0]:
+            best = (th, e, col, Rc, ax)
+    th, e, col, Rc, ax = best
+    x[col:col + 3] = N.log_so3(Rc.T @ _rot(ax, np.pi)).astype(np.float32)
+    R3 = Rc @ N.rodrigues(x[col:col + 3].astype(np.float64))
+    s = abs(np.sin(np.linalg.norm(N.log_so3(R3))))
+    return p, x, e, s, th
+
+
+@pytest.fixture(scope="module")
+def host():
+    api.build()
+    api.lib()
+    import ctypes
+    L = ctypes.CDLL(api.HOST_LIB_PATH)
+    _d = ctypes.POINTER(ctypes.c_double)
+    _f = ctypes.POINTER(ctypes.c_float)
+    L.mcc_host_edge_jacobian.argtypes = [ctypes.c_int] * 3 + [_d] * 6 + [ctypes.c_int, _f, _f, _f, _f, ctypes.c_int,
+                                                                         ctypes.c_float, _d, _d, _d, _f]
+    return L
+
+
+@pytest.mark.parametrize("model", ["doubleside", "mymulti_back"])
+def test_host_edge_jacobian_in_the_branch(host, model):
+    import test_edge_jacobian as T
+    p, x, e, s, th0 = _branch_problem(model)
+    assert s < 1e-5, (s, th0)
+    jc_o, jp_o, _, _ = O.Oracle(p).edge_linearize(x, e)
+    assert np.abs(jp_o[:, :3]).max() == 0.0   # the reference: no rotation columns for the photo
+    T._check_problem(host, p, x, model)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,env", [
+    ("doubleside", {"MCC_FUSED": "1"}), ("doubleside", {"MCC_FUSED": "0", "MCC_GROUP": "1"}),
+    ("doubleside", {"MCC_FUSED": "0", "MCC_GROUP": "0"}),
+    ("mymulti_back", {"MCC_FUSED": "1"}), ("mymulti_back", {"MCC_FUSED": "0", "MCC_GROUP": "1"}),
+    ("mymulti_back", {"MCC_FUSED": "0", "MCC_GROUP": "0"})],
+    ids=["ds_fused", "ds_group", "ds_split3", "back_fused", "back_group", "back_split3"])
+def test_gpu_linearize_in_the_branch(model, env):
+    p, x, e, s, _ = _branch_problem(model)
+    assert s < 1e-5
+    o = O.Oracle(p)
+    d_ref, j_ref = o.linearize_solve(x, "schur")
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        g = api.BundleAdjuster(p)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        d, j = g.compute_jacobian_extrinsic(x)
+    finally:
+        g.close()
+    assert np.abs(j - j_ref).max() <= 1e-9 * np.abs(j_ref).max(), np.abs(j - j_ref).max() / np.abs(j_ref).max()
+    assert np.abs(d - d_ref).max() <= 1e-6 * np.abs(d_ref).max(), np.abs(d - d_ref).max() / np.abs(d_ref).max()
