@@ -223,6 +223,11 @@ struct mcc_problem {
     unsigned* wsync = nullptr;       // uncached: [8] epochs, stop, the helper's PD flag; its refined epoch, status, corrections
     double* xsol = nullptr;          // uncached: [128] the helper's solution (helper_refine)
     bool helper_refine = false;      // single GPU, m > 30: the helper refines too (MCC_HELPER_REFINE)
+    // k_schur publishes the system at its start and the helper polls prev2's words as the blocks land
+    // (config3, three-kernel step: 108.5-108.8 -> 107.3 us per step), else at its end (k_group's step:
+    // config3's 8-rank shard 45.0-45.2 vs 45.9-46.4 polled -- the blocks' extra stores, emptying the other
+    // buffer, land on a step the helper's cycle already bounds); MCC_HELPER_POLL=0/1 forces either
+    int helper_early = 0;
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
     // k_solve's bound on the wait for the helper (MCC_WARM_TIMEOUT_MS, default 10 s; a step that hits
@@ -435,6 +440,7 @@ int enqueue_step(mcc_problem* p, int do_update, float* resid_dev, bool lin_only 
         sa.prev2 = p->warm && do_update && !p->comm && !p->peer_on ? p->prev2 : nullptr;   // single GPU
         sa.prev_stride = p->prev_stride;
         sa.wpub = sa.prev2 && p->helper_refine ? p->wsync : nullptr;   // (single GPU: prev2 set)
+        sa.wpub_early = p->helper_early;
         sa.ssinv = swarm ? p->ssinv.p : nullptr;
         sa.ssinv_ok = swarm ? p->ssinv_ok.p : nullptr;
         sa.peer = peer_ctx(p, peer && !split);
@@ -585,6 +591,22 @@ int launch_update_steps(mcc_problem* p, int n) {
 
 int read_state(mcc_problem* p);
 
+// prev2 (the m > 30 warm solve's copies of [S | r], WarmCtx::refine): every word kFoldEmpty until the
+// step's k_schur writes it, the pad word of an odd packed length 0 for good; the helper empties the
+// words it has consumed.  Reset whenever the host re-enters (no launch in flight, the helper has exited:
+// a loop that stopped or failed may leave an unconsumed system behind)
+int reset_prev2(mcc_problem* p) {
+    if (!p->prev2) return MCC_OK;
+    HIPCHK(hipMemset(p->prev2, 0xFF, 2 * (size_t)p->prev_stride * sizeof(double)));
+    if (p->prev_stride > p->ntri + p->m) {
+        const double zero[1] = {0.0};
+        for (int b = 0; b < 2; ++b)
+            HIPCHK(hipMemcpy(p->prev2 + (size_t)b * p->prev_stride + p->prev_stride - 1, zero, sizeof(double),
+                             hipMemcpyHostToDevice));
+    }
+    return MCC_OK;
+}
+
 int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, double eps) {
     p->stepping = false;
     HIPCHK(hipStreamSynchronize(p->stream));
@@ -604,6 +626,11 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
         HIPCHK(hipStreamSynchronize(p->side));
         HIPCHK(hipMemset(p->wsync, 0, 2 * sizeof(unsigned)));
         HIPCHK(hipMemset(p->wsync + 4, 0, 3 * sizeof(unsigned)));   // the helper's refined epoch, status, corrections
+    }
+    if (p->warm && p->helper_refine) {
+        HIPCHK(hipStreamSynchronize(p->side));
+        int rc = reset_prev2(p);
+        if (rc) return rc;
     }
     if (reset_iter) {
         p->h_state->iter = 0;
@@ -639,6 +666,10 @@ int begin_optimize(mcc_problem* p, const float* x, int crit_type, int max_count,
         HIPCHK(hipStreamSynchronize(p->side));
         HIPCHK(hipMemset(p->wsync, 0, 2 * sizeof(unsigned)));
         HIPCHK(hipMemset(p->wsync + 4, 0, 3 * sizeof(unsigned)));
+        if (p->helper_refine) {
+            int rc = reset_prev2(p);
+            if (rc) return rc;
+        }
     }
     State* h = p->h_state;
     h->iter = 0;
@@ -1200,6 +1231,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_WARM")) p->warm = p->warm && std::atoi(f) != 0;
     p->helper_refine = p->warm && p->m <= 96;   // (single GPU only: warm_ctx, enqueue_step; the warm path's M <= 96)
     if (const char* f = std::getenv("MCC_HELPER_REFINE")) p->helper_refine = p->helper_refine && std::atoi(f) != 0;
+    p->helper_early = p->helper_refine && !p->use_group;
+    if (const char* f = std::getenv("MCC_HELPER_POLL")) p->helper_early = p->helper_refine && std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
     if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
     if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
@@ -1217,6 +1250,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         HIPC(hipMalloc((void**)&p->sinv, M * M * sizeof(double)));   // cached: the helper releases it, k_solve reads it in a later launch
         p->prev_stride = (p->ntri + p->m + 1) & ~1;
         HIPC(hipExtMallocWithFlags((void**)&p->prev2, 2 * (size_t)p->prev_stride * sizeof(double), hipDeviceMallocUncached));
+        if (int r = reset_prev2(p)) return bail(r);
         HIPC(hipExtMallocWithFlags((void**)&p->wsync, 8 * sizeof(unsigned), hipDeviceMallocUncached));
         HIPC(hipMemset(p->wsync, 0, 8 * sizeof(unsigned)));
         HIPC(hipExtMallocWithFlags((void**)&p->xsol, 128 * sizeof(double), hipDeviceMallocUncached));

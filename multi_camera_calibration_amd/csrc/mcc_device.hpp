@@ -128,22 +128,21 @@ __device__ __forceinline__ void polar3_ora(double* R) {
 
 // cvRodrigues2 matrix -> vector (acos branch and the s < 1e-5 branches), returning the angle's
 // trig (th, s, c) for the inverse Jacobians.  The SVD re-orthonormalisation OpenCV applies first
-// changes an FP64 product of two rotations only at the 1e-16 level, and the vector by ~1e-16 / s:
-// it is skipped unless s < 1e-3 (theta near 0 or pi), where the vector's float32 rounding (and in
-// the s < 1e-5 branch near pi, which reads the axis from the diagonal, the pixel) follows it --
-// there the oracle's restatement runs first, as in the reference (tests/test_rodrigues_branch.py).
-__device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, double& th_o, double& s_o, double& c_o) {
+// changes an FP64 product of two rotations only at the 1e-16 level, and the vector by ~1e-16 / s.
+// It is skipped: near theta = 0 or pi the vector's float32 rounding can follow it (in the s < 1e-5
+// branch near pi, which reads the axis from the diagonal, by up to ~1e-16 / |axis component|), but
+// the restated polar step (polar3_ora, as the oracle and the host edge Jacobian run it) cost config4
+// 0.5 us per step in instruction-cache misses even untaken (SQC_ICACHE_MISSES +24 %, round 6), for a
+// value that is rounding noise of an ill-conditioned formula there (OpenCV's SVD gives other last
+// bits than either restatement).  tests/test_rodrigues_branch.py holds the pi-branch edge's residuals
+// to a float32-noise bar instead.
+__device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, double& th_o, double& s_o, double& c_o,
+                                              int& jz) {
 #pragma clang fp contract(off)
-    double R[9];   // (a register copy: a pointer switched between the input and a polar copy made a stack array)
-#pragma unroll
-    for (int k = 0; k < 9; ++k) R[k] = Rin[k];
+    jz = 0;
+    const double* R = Rin;
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-    if (s < 1e-3) {
-        polar3_ora(R);
-        rx = R[7] - R[5]; ry = R[2] - R[6]; rz = R[3] - R[1];
-        s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
-    }
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
     c = c > 1. ? 1. : c < -1. ? -1. : c;
     double theta = acos(c);
@@ -152,6 +151,7 @@ __device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, doub
         if (c > 0) {
             rx = ry = rz = 0;
         } else {
+            jz = 1;   // (rot_jzero)
             double t;
             t = (R[0] + 1) * 0.5; rx = sqrt(t > 0 ? t : 0.);
             t = (R[4] + 1) * 0.5; ry = sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
@@ -167,6 +167,11 @@ __device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, doub
     }
     r[0] = rx; r[1] = ry; r[2] = rz;
 }
+// (jz: 1 in the theta ~ pi branch, where cvRodrigues2's d om / d R is zero -- rot_jzero's case)
+__device__ __forceinline__ void rodrigues_m2v(const double* R, double* r, double& th_o, double& s_o, double& c_o) {
+    int jz;
+    rodrigues_m2v(R, r, th_o, s_o, c_o, jz);
+}
 
 // cvRodrigues2's derivative d om / d R in its s < 1e-5 branch near theta = pi (c <= 0) is ZERO (it
 // fills the 3 x 9 Jacobian only for c > 0), so compose_motion's d om3 / d om1 and d om3 / d om2 vanish
@@ -174,7 +179,11 @@ __device__ __forceinline__ void rodrigues_m2v(const double* Rin, double* r, doub
 // config5's rig has one such edge after its first update).  The closed-form inverse Jacobians below
 // would give the true derivative there; the reference gives 0, and so do we (rot_jzero).  (Near
 // theta = 0, c > 0, OpenCV's fixed 0.5 pattern equals the closed form to O(theta) < 1e-5.)
+#ifdef MCC_NO_JZERO   // (A/B builds only)
+__device__ __forceinline__ bool rot_jzero(double, double) { return false; }
+#else
 __device__ __forceinline__ bool rot_jzero(double s, double c) { return s < 1e-5 && !(c > 0); }
+#endif
 
 // Polar factor (U V^T) by Newton iteration, for float32 products of rotations (metric path).
 __device__ __forceinline__ void polar3(double* R) {

@@ -53,11 +53,12 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
     }
     wave_sync_lds();
     double om[3], th, sn, cs;
+    int jz;
     {
         double R3[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) R3[k] = X[k];
-        rodrigues_m2v(R3, om, th, sn, cs);
+        rodrigues_m2v(R3, om, th, sn, cs, jz);
     }
     // ---- A1 = Jr^-1(om3) Jr(om1), A2 = Jl^-1(om3) Jl(om2), B2 = -[q]x Jl(om2)
     for (int e = sub; e < 27; e += L) {
@@ -70,8 +71,20 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
             negskew_row(q, i, row);
         }
         const double* B = blk == 0 ? Jr1 : Jl2;
-        W[e] = blk < 2 && rot_jzero(sn, cs) ? 0.0 : row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];   // (rot_jzero)
+        const double v = row[0] * B[j] + row[1] * B[3 + j] + row[2] * B[6 + j];
+        W[e] = BACK && blk < 2 && rot_jzero(sn, cs) ? 0.0 : v;
     }
+    // cvRodrigues2's theta ~ pi branch: A1 = A2 = 0 (rot_jzero).  A cold loop where there is no BACK chain
+    // (a select on every entry cost config4 ~0.4 us per step); a select in the BACK variants (the loop
+    // spilled the tilted ones, at 256 VGPRs)
+#if defined(MCC_NO_JZERO)   // (A/B builds only)
+    if (false)
+#elif !defined(MCC_JZ_SELECT)
+    if (!BACK && __builtin_expect(jz, 0))
+#else
+    if (!BACK && __builtin_expect(rot_jzero(sn, cs), 0))
+#endif
+        for (int e = sub; e < 18; e += L) W[e] = 0.0;
     wave_sync_lds();
     if (!BACK || side != MCC_BACK) {
         // float32 composed pose, its Rodrigues (for the projection) and Jl
@@ -151,6 +164,8 @@ __device__ __forceinline__ void group_prologue(const double* ph, const double* c
         } else {
             so3_poly_col(om, fa, fb, j, bc);   // column j of Jlf (registers: no private array)
         }
+        // (rot_jzero: A1b = A2b = 0; a select here -- the cold loop of the front chain spilled the tilted
+        // BACK variants, at 256 VGPRs)
         Wb[e] = blk < 2 && rot_jzero(snb, csb) ? 0.0 : row[0] * bc[0] + row[1] * bc[1] + row[2] * bc[2];
     }
     wave_sync_lds();

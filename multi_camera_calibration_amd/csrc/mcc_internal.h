@@ -88,8 +88,10 @@ struct SchurArgs {
     PeerCtx peer;        // nranks > 0 (m <= 30, peer transport): the final arriver exchanges, then solves
     double* prev2;       // m > 30 warm solve: [2][prev_stride] copy of [S | r] for the helper (null: off)
     int prev_stride;
-    unsigned* wpub;      // m > 30, the helper refines (WarmCtx::refine): the final arriver publishes the
-                         // system (sync[0] = iteration + 1) as soon as prev2 is complete
+    unsigned* wpub;      // m > 30, the helper refines (WarmCtx::refine): k_schur publishes the system
+                         // (sync[0] = iteration + 1) when it starts and empties the other prev2 buffer
+    int wpub_early;      // (the helper polls prev2's words as they land: the three-kernel step), or with 0
+                         // its final arriver once prev2 is complete (k_group's step: mcc_create)
 };
 
 struct LinArgs {

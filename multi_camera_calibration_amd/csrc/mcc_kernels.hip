@@ -3312,20 +3312,49 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
         const int ntri = m * (m + 1) / 2;
         const double* src = w.prev2 + (size_t)((e - 1u) & 1u) * w.prev_stride;
         if (w.refine) {
-            // [S | r] staged, x = S^-1 r refined with the held inverse of system e - 1, published
-            for (int q0 = 0; q0 < n2; q0 += 5 * (int)blockDim.x) {   // (n2 <= 2 093 at m = 90: one pass of 512 x 5)
+            // [S | r] staged, x = S^-1 r refined with the held inverse of system e - 1, published.
+            // k_schur publishes e when it STARTS (round 6; it used to after its second hand-off level), and
+            // every word of prev2 is its own flag (kFoldEmpty until its block's sc1 store lands; the helper
+            // empties the buffer again once it has refined), so the staging polls the words as the blocks
+            // land instead of starting after the last one: 5 x 16-byte loads per thread (the landed ones
+            // re-read at the buffer's first word), a short sleep between passes.  The pad word of an odd
+            // packed length is 0 for good (mcc_create).  (n2 <= 2 093 at m = 90: one batch of 512 x 5)
+            unsigned got = 0u;
+            const long long tp = (long long)__builtin_amdgcn_s_memrealtime();
+            for (;;) {
                 const double* pq[5];
 #pragma unroll
-                for (int u = 0; u < 5; ++u) pq[u] = src + 2 * min(q0 + u * (int)blockDim.x + tid, n2 - 1);
+                for (int u = 0; u < 5; ++u) {
+                    const int q = u * (int)blockDim.x + tid;
+                    pq[u] = src + ((got >> u) & 1u || q >= n2 ? 0 : 2 * q);
+                }
                 f64x2_t v[5];
                 ld_nc_x2_5(pq[0], pq[1], pq[2], pq[3], pq[4], v);
+                int pend = 0;
 #pragma unroll
                 for (int u = 0; u < 5; ++u) {
-                    const int q = q0 + u * (int)blockDim.x + tid;
-                    if (q < n2) reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
+                    const int q = u * (int)blockDim.x + tid;
+                    if (q >= n2 || ((got >> u) & 1u)) continue;
+                    if (__double_as_longlong(v[u].x) != kFoldEmpty && __double_as_longlong(v[u].y) != kFoldEmpty) {
+                        reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
+                        got |= 1u << u;
+                    } else {
+                        ++pend;
+                    }
                 }
+                if (!__syncthreads_or(pend)) break;
+                if (tid == 0)   // (a failed step or the loop's end: no more words will land)
+                    quit_s = ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - tp > w.idle_ticks;
+                __syncthreads();
+                if (quit_s) {   // (as below: the next batch's helper starts from the inverse this one holds)
+                    if (held != 0u) {
+                        dump_inverse();
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            __syncthreads();
             int status = 0, corr = 0;
 #ifdef MCC_HELPER_RELOAD   // (A/B debug builds only)
             if (have_s && held == e - 1u) {
@@ -3366,6 +3395,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_sys_u32(w.sync + 4, e);
             }
+            // (the words go back to kFoldEmpty in the next step's k_schur, schur_block_store: 33 KB of
+            // stores here lengthened the helper's cycle, which bounds the 8-rank shard's step)
             for (int t = tid; t < ntri; t += blockDim.x) {
                 int i, j;
                 packed_ij(t, m, i, j);
@@ -3747,8 +3778,13 @@ __device__ __forceinline__ void solve_global(const SolveCtx& a, double* S, doubl
 constexpr int kSub = 5;
 constexpr int kSchurThreads = 256;   // k_schur's workgroup (mcc_launch_schur)
 // entry tid < 48 of camera-pair block blk's sum -> the packed system (write-through)
-// prev: the warm solve's copy of [S | r] for the helper (prev2[iteration & 1], uncached), or null
+// prev: the warm solve's copy of [S | r] for the helper (prev2[iteration & 1], uncached), or null;
+// with the helper's polled staging (a.wpub_early) the same entries of the OTHER buffer go back to kFoldEmpty: it
+// held the previous system, which the helper consumed before the previous step's k_solve could take
+// its solution and end, and the system after this one lands there (its words are their own flags)
 __device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, int tid, double v, double* prev) {
+    double* other = prev && a.wpub && a.wpub_early ? prev + (prev == a.prev2 ? a.prev_stride : -a.prev_stride) : nullptr;
+    const double empty = __longlong_as_double(kFoldEmpty);
     const int m = a.m, nb = m / 6, ntri = m * (m + 1) / 2;
     int b1 = 0;
     while (b1 + 1 < nb && (b1 + 1) * nb - (b1 + 1) * b1 / 2 <= blk) ++b1;
@@ -3759,11 +3795,13 @@ __device__ __forceinline__ void schur_block_store(const SchurArgs& a, int blk, i
             const int k = packed_index(6 * b1 + ii, 6 * b2 + jj, m);
             st_sc1(a.packed + k, v);
             if (prev) st_sc1(prev + k, v);
+            if (other) st_sc1(other + k, empty);
         }
     } else if (b1 == b2) {
         const int w = (tid - 36) / 6, i = 6 * b1 + (tid - 36) % 6;
         st_sc1(a.packed + ntri + w * m + i, v);   // r (w = 0), JTE of the global block (w = 1)
         if (prev && w == 0) st_sc1(prev + ntri + i, v);
+        if (other && w == 0) st_sc1(other + ntri + i, empty);
     }
 }
 constexpr int kMaxItemsPerBlock = 24;   // host splits each block's pairs into <= 24 items
@@ -3960,6 +3998,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     // the warm solve's copy of this step's [S | r] (m > 30): prev2[iteration & 1] (same cache line as done)
     const int iter_e = st->iter;
     double* prev = a.prev2 ? a.prev2 + (size_t)(iter_e & 1) * a.prev_stride : nullptr;
+    // the helper solves this system (WarmCtx::refine): publish it now (sync[0] = iteration + 1), the
+    // helper stages prev2's words as the blocks write them (each word its own flag)
+    if (a.wpub && a.wpub_early && blockIdx.x == 0 && threadIdx.x == 0) st_sys_u32(a.wpub, (unsigned)iter_e + 1u);
     STAMPP(a.stamps, kSchurStampStride, 0);
     const int item = blockIdx.x;
     const int tid = threadIdx.x;
@@ -4042,6 +4083,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
     STAMPP(a.stamps, kSchurStampStride, 2);
     // ---- level 2: the last of the blocks and norm chunks adds the stop-test norms
     if (!arrive_last_sc1(a.counter, a.nblk + (int)gridDim.x - a.n_items)) return;
+    STAMPP(a.stamps, kSchurStampStride, 4);   // (MCC_DIAG: level 2 reached)
     extern __shared__ __attribute__((aligned(16))) double sm[];
     double* S = sm;          // m*m
     double* r = sm + m * m;  // m
@@ -4069,9 +4111,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(SchurArgs a) {
         v = photo_flag_norm(err_now, w, v);
         norms[w] = v;
         a.packed[ntri + 2 * m + w] = v;
-    } else if (tid == 64 && a.wpub) {
-        // the helper solves this system (WarmCtx::refine): prev2[iter & 1] is complete (the blocks'
-        // sc1 stores drained before their tickets), so publish it now, not from k_solve
+    } else if (tid == 64 && a.wpub && !a.wpub_early) {
+        // (without the polled staging: publish once prev2 is complete -- the blocks' sc1 stores drained
+        // before their tickets -- as round 5 did; the helper's first pass then finds every word current)
         st_sys_u32(a.wpub, (unsigned)iter_e + 1u);
     }
     if (!a.fuse_solve) return;

@@ -14,7 +14,7 @@ JTE differed from the oracle's by 3e-4 relative there and the final iterate by 4
     closed form's elsewhere; the host per-edge Jacobian (libmcc_host.so) matches the oracle on an edge
     moved into the branch;
   * GPU: every step path (fused, k_group, three-kernel) matches the oracle's JTE and solved step on a
-    DoubleSide rig with one photo moved so that an edge lands in the branch.
+    DoubleSide and a MyMulti BACK rig with one photo moved so that an edge lands in the branch.
 """
 import os
 import sys
@@ -131,7 +131,26 @@ def test_gpu_linearize_in_the_branch(model, env):
                 os.environ[k] = v
     try:
         d, j = g.compute_jacobian_extrinsic(x)
+        r = g.residuals(x)
     finally:
         g.close()
-    assert np.abs(j - j_ref).max() <= 1e-9 * np.abs(j_ref).max(), np.abs(j - j_ref).max() / np.abs(j_ref).max()
-    assert np.abs(d - d_ref).max() <= 1e-6 * np.abs(d_ref).max(), np.abs(d - d_ref).max() / np.abs(d_ref).max()
+    # float32 residuals bitwise up to 1-ulp FP64 ties (tests/test_gpu_parity.py::test_residuals_bitwise),
+    # except on the pi-branch edge: its pose vector comes from the diagonal formula, which turns the
+    # 1e-16 non-orthogonality of the composed FP64 rotation into ~1e-16 / |axis component| -- OpenCV
+    # re-orthonormalises first (SVD), the oracle and the host by a Newton polar step, the device not
+    # (mcc_device.hpp rodrigues_m2v: untaken, that code cost config4 0.5 us per step).  There the bar is
+    # float32 noise of the pixel, 1e-3 px, and JTE / Delta take that edge's J x that difference.
+    ref = np.concatenate([o.edge_linearize(x, k)[2] for k in range(p.n_edges)]).astype(np.float32)
+    eo = np.repeat(np.arange(p.n_edges), 2 * p.edge_n)
+    diff = (r != ref) & (eo != e)
+    assert diff.sum() <= 2, int(diff.sum())
+    if diff.any():
+        assert np.abs(r[diff].view(np.int32).astype(np.int64) - ref[diff].view(np.int32)).max() <= 1
+    on = eo == e
+    noise = float(np.abs(r[on].astype(np.float64) - ref[on]).max())
+    assert noise <= 1e-3, noise
+    bar_j, bar_d = (1e-9, 1e-6) if noise == 0.0 and not diff.any() else (1e-7, 1e-5)
+    assert np.abs(j - j_ref).max() <= bar_j * np.abs(j_ref).max(), (noise, np.abs(j - j_ref).max() / np.abs(j_ref).max())
+    assert np.abs(d - d_ref).max() <= bar_d * np.abs(d_ref).max(), (noise, np.abs(d - d_ref).max() / np.abs(d_ref).max())
+    # the reference's zero rotation partials: without them the photo's JTE moved by ~1e-4 relative
+    # (config5 at its first update, tools/diverge.py), far above these bars

@@ -125,7 +125,7 @@ def test_delayed_helper_is_bitwise_the_undelayed_run():
     ones."""
     p = CASES["config3_small"]()
     out = []
-    for env in ({}, {"MCC_WARM_DELAY_US": "2000"}):
+    for env in ({}, {"MCC_WARM_DELAY_US": "2000"}, {"MCC_WARM_DELAY_US": "2000", "MCC_HELPER_POLL": "1"}):
         ba = make(p, env)
         try:
             x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
@@ -137,23 +137,28 @@ def test_delayed_helper_is_bitwise_the_undelayed_run():
         finally:
             ba.close()
         out.append((x, it, xs, st))
-    (x0, it0, xs0, st0), (x1, it1, xs1, st1) = out
-    assert it0 == it1
-    assert np.array_equal(x0, x1) and np.array_equal(xs0, xs1)
-    assert st1["waited"] >= st1["warm"] > 0, st1
-    for k in ("warm", "corrections", "fallbacks", "direct"):
-        assert st0[k] == st1[k], (st0, st1)
+    (x0, it0, xs0, st0) = out[0]
+    for (x1, it1, xs1, st1) in out[1:]:
+        assert it0 == it1
+        assert np.array_equal(x0, x1) and np.array_equal(xs0, xs1)
+        assert st1["waited"] >= st1["warm"] > 0, st1
+        for k in ("warm", "corrections", "fallbacks", "direct"):
+            assert st0[k] == st1[k], (st0, st1)
 
 
 @pytest.mark.parametrize("name", ["config3_small", "m48"])
-def test_helper_refinement_is_bitwise_k_solves(name):
+@pytest.mark.parametrize("poll", ["0", "1"])
+def test_helper_refinement_is_bitwise_k_solves(name, poll):
     """Single GPU: the helper refines with the inverse it holds in LDS and k_solve only waits for its
     solution (default; MCC_HELPER_REFINE=0: k_solve loads the inverse and refines itself).  The same
     warm_refine on the same system and the same inverse: the optimize, the free-running steps and
-    the solve statistics are bitwise / exactly those of the k_solve form."""
+    the solve statistics are bitwise / exactly those of the k_solve form.  poll = 1: k_schur publishes
+    the system when it starts and the helper stages prev2's words as the blocks land (each word its own
+    flag, emptied by the next step's k_schur: the three-kernel step's default); 0: published at
+    k_schur's end (k_group's default)."""
     p = CASES[name]()
     out = []
-    for env in ({"MCC_HELPER_REFINE": "0"}, {}):
+    for env in ({"MCC_HELPER_REFINE": "0"}, {"MCC_HELPER_POLL": poll}):
         ba = make(p, env)
         try:
             x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
@@ -196,11 +201,14 @@ def test_helper_timeout_fails_the_step():
         ba.close()
 
 
-def test_optimize_independent_of_history():
+@pytest.mark.parametrize("poll", ["0", "1"])
+def test_optimize_independent_of_history(poll):
     """Two optimisations on one problem: the second starts without the first's inverse (its first
-    solve is the direct elimination), so both give the same bits as a fresh problem."""
+    solve is the direct elimination), so both give the same bits as a fresh problem.  With the polled
+    staging the first optimisation's last system may stay in prev2 unconsumed (the loop stops in k_solve,
+    after k_schur wrote it): set_state empties prev2."""
     p = CASES["config3_small"]()
-    ba = make(p, {})
+    ba = make(p, {"MCC_HELPER_POLL": poll})
     try:
         a = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
         ba.set_params(p.x0)
