@@ -224,9 +224,9 @@ struct mcc_problem {
     double* xsol = nullptr;          // uncached: [128] the helper's solution (helper_refine)
     bool helper_refine = false;      // single GPU, m > 30: the helper refines too (MCC_HELPER_REFINE)
     // k_schur publishes the system at its start and the helper polls prev2's words as the blocks land
-    // (config3, three-kernel step: 108.5-108.8 -> 107.3 us per step), else at its end (k_group's step:
-    // config3's 8-rank shard 45.0-45.2 vs 45.9-46.4 polled -- the blocks' extra stores, emptying the other
-    // buffer, land on a step the helper's cycle already bounds); MCC_HELPER_POLL=0/1 forces either
+    // (config3, three-kernel step: 108.4-109.1 -> 107.4-107.6 us per step), else at its end and the helper
+    // stages in one batch (k_group's step: config3's 8-rank shard, whose step the helper's cycle bounds,
+    // was 0.9 us slower polled); MCC_HELPER_POLL=0/1 forces either
     int helper_early = 0;
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
@@ -325,7 +325,7 @@ mcc::WarmCtx warm_ctx(mcc_problem* p) {
     const int copy_prev = (p->comm || p->peer_on) ? 1 : 0;   // sharded: k_solve copies the summed system
     return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->prev2, p->prev_stride, copy_prev, p->wsync, p->warm_stats.p,
                         p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks,
-                        p->helper_refine && !copy_prev ? 1 : 0, p->xsol};
+                        p->helper_refine && !copy_prev ? 1 : 0, p->xsol, p->helper_early};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {

@@ -324,6 +324,8 @@ struct WarmCtx {
     int refine;              // single GPU (MCC_HELPER_REFINE): the helper refines with the inverse it holds in
                              // LDS and publishes x (xsol); k_solve only waits for it (or eliminates)
     double* xsol;            // refine: [kWarmN] uncached, the helper's solution of the published system
+    int poll;                // refine: k_schur publishes at its start and the helper polls prev2's words
+                             // (SchurArgs::wpub_early), else one batch once the system is complete
 };
 constexpr int kWarmMaxIters = 4;
 

@@ -3319,41 +3319,58 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
             // land instead of starting after the last one: 5 x 16-byte loads per thread (the landed ones
             // re-read at the buffer's first word), a short sleep between passes.  The pad word of an odd
             // packed length is 0 for good (mcc_create).  (n2 <= 2 093 at m = 90: one batch of 512 x 5)
-            unsigned got = 0u;
-            const long long tp = (long long)__builtin_amdgcn_s_memrealtime();
-            for (;;) {
-                const double* pq[5];
+            if (!w.poll) {   // (published complete: round 5's one batch -- the polling loop below cost the
+                             // 8-rank shard, whose step the helper's cycle bounds, 0.9 us even in one pass)
+                for (int q0 = 0; q0 < n2; q0 += 5 * (int)blockDim.x) {
+                    const double* pq[5];
 #pragma unroll
-                for (int u = 0; u < 5; ++u) {
-                    const int q = u * (int)blockDim.x + tid;
-                    pq[u] = src + ((got >> u) & 1u || q >= n2 ? 0 : 2 * q);
-                }
-                f64x2_t v[5];
-                ld_nc_x2_5(pq[0], pq[1], pq[2], pq[3], pq[4], v);
-                int pend = 0;
+                    for (int u = 0; u < 5; ++u) pq[u] = src + 2 * min(q0 + u * (int)blockDim.x + tid, n2 - 1);
+                    f64x2_t v[5];
+                    ld_nc_x2_5(pq[0], pq[1], pq[2], pq[3], pq[4], v);
 #pragma unroll
-                for (int u = 0; u < 5; ++u) {
-                    const int q = u * (int)blockDim.x + tid;
-                    if (q >= n2 || ((got >> u) & 1u)) continue;
-                    if (__double_as_longlong(v[u].x) != kFoldEmpty && __double_as_longlong(v[u].y) != kFoldEmpty) {
-                        reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
-                        got |= 1u << u;
-                    } else {
-                        ++pend;
+                    for (int u = 0; u < 5; ++u) {
+                        const int q = q0 + u * (int)blockDim.x + tid;
+                        if (q < n2) reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
                     }
                 }
-                if (!__syncthreads_or(pend)) break;
-                if (tid == 0)   // (a failed step or the loop's end: no more words will land)
-                    quit_s = ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - tp > w.idle_ticks;
                 __syncthreads();
-                if (quit_s) {   // (as below: the next batch's helper starts from the inverse this one holds)
-                    if (held != 0u) {
-                        dump_inverse();
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                unsigned got = 0u;
+                const long long tp = (long long)__builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    const double* pq[5];
+#pragma unroll
+                    for (int u = 0; u < 5; ++u) {
+                        const int q = u * (int)blockDim.x + tid;
+                        pq[u] = src + ((got >> u) & 1u || q >= n2 ? 0 : 2 * q);
                     }
-                    return;
+                    f64x2_t v[5];
+                    ld_nc_x2_5(pq[0], pq[1], pq[2], pq[3], pq[4], v);
+                    int pend = 0;
+#pragma unroll
+                    for (int u = 0; u < 5; ++u) {
+                        const int q = u * (int)blockDim.x + tid;
+                        if (q >= n2 || ((got >> u) & 1u)) continue;
+                        if (__double_as_longlong(v[u].x) != kFoldEmpty && __double_as_longlong(v[u].y) != kFoldEmpty) {
+                            reinterpret_cast<double2*>(Pk)[q] = make_double2(v[u].x, v[u].y);
+                            got |= 1u << u;
+                        } else {
+                            ++pend;
+                        }
+                    }
+                    if (!__syncthreads_or(pend)) break;
+                    if (tid == 0)   // (a failed step or the loop's end: no more words will land)
+                        quit_s = ld_sys_u32(w.sync + 2) || (long long)__builtin_amdgcn_s_memrealtime() - tp > w.idle_ticks;
+                    __syncthreads();
+                    if (quit_s) {   // (as below: the next batch's helper starts from the inverse this one holds)
+                        if (held != 0u) {
+                            dump_inverse();
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        }
+                        return;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
             int status = 0, corr = 0;
 #ifdef MCC_HELPER_RELOAD   // (A/B debug builds only)
