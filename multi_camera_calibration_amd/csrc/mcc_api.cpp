@@ -595,14 +595,18 @@ int read_state(mcc_problem* p);
 // step's k_schur writes it, the pad word of an odd packed length 0 for good; the helper empties the
 // words it has consumed.  Reset whenever the host re-enters (no launch in flight, the helper has exited:
 // a loop that stopped or failed may leave an unconsumed system behind)
-int reset_prev2(mcc_problem* p) {
+// (stream-ordered on the step stream: k_schur's writes follow it, and the helper reads a buffer only
+// after k_schur's publication; `pad_too` also sets the pad words, once at mcc_create)
+int reset_prev2(mcc_problem* p, bool pad_too = false) {
     if (!p->prev2) return MCC_OK;
-    HIPCHK(hipMemset(p->prev2, 0xFF, 2 * (size_t)p->prev_stride * sizeof(double)));
-    if (p->prev_stride > p->ntri + p->m) {
+    const int n = p->ntri + p->m;   // the words k_schur writes; the pad word after them stays 0
+    for (int b = 0; b < 2; ++b)
+        HIPCHK(hipMemsetAsync(p->prev2 + (size_t)b * p->prev_stride, 0xFF, (size_t)n * sizeof(double), p->stream));
+    if (pad_too && p->prev_stride > n) {
+        HIPCHK(hipStreamSynchronize(p->stream));
         const double zero[1] = {0.0};
         for (int b = 0; b < 2; ++b)
-            HIPCHK(hipMemcpy(p->prev2 + (size_t)b * p->prev_stride + p->prev_stride - 1, zero, sizeof(double),
-                             hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(p->prev2 + (size_t)b * p->prev_stride + n, zero, sizeof(double), hipMemcpyHostToDevice));
     }
     return MCC_OK;
 }
@@ -631,6 +635,13 @@ int set_state(mcc_problem* p, int reset_iter, int crit_type, int max_count, doub
         HIPCHK(hipStreamSynchronize(p->side));
         int rc = reset_prev2(p);
         if (rc) return rc;
+        if (!reset_iter) {
+            // a system the last batch's helper did not consume (the loop stopped in k_solve after k_schur
+            // published it) is withdrawn with its words: the next helper waits for the next publication
+            unsigned inv = 0;
+            HIPCHK(hipMemcpy(&inv, p->wsync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(p->wsync, &inv, sizeof(unsigned), hipMemcpyHostToDevice));
+        }
     }
     if (reset_iter) {
         p->h_state->iter = 0;
@@ -1250,7 +1261,7 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
         HIPC(hipMalloc((void**)&p->sinv, M * M * sizeof(double)));   // cached: the helper releases it, k_solve reads it in a later launch
         p->prev_stride = (p->ntri + p->m + 1) & ~1;
         HIPC(hipExtMallocWithFlags((void**)&p->prev2, 2 * (size_t)p->prev_stride * sizeof(double), hipDeviceMallocUncached));
-        if (int r = reset_prev2(p)) return bail(r);
+        if (int r = reset_prev2(p, true)) return bail(r);
         HIPC(hipExtMallocWithFlags((void**)&p->wsync, 8 * sizeof(unsigned), hipDeviceMallocUncached));
         HIPC(hipMemset(p->wsync, 0, 8 * sizeof(unsigned)));
         HIPC(hipExtMallocWithFlags((void**)&p->xsol, 128 * sizeof(double), hipDeviceMallocUncached));
