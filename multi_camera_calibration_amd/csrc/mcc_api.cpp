@@ -228,6 +228,7 @@ struct mcc_problem {
     // stages in one batch (k_group's step: config3's 8-rank shard, whose step the helper's cycle bounds,
     // was 0.9 us slower polled); MCC_HELPER_POLL=0/1 forces either
     int helper_early = 0;
+    int inv_la = 0;                  // the helper's look-ahead inversion (WarmCtx::inv_la): the k_group path
     DevBuf<long long> warm_stats;    // [5] (mcc_solve_stats)
     int warm_poison = 0;             // MCC_WARM_POISON=1 (test): the helper publishes NaN inverses
     // k_solve's bound on the wait for the helper (MCC_WARM_TIMEOUT_MS, default 10 s; a step that hits
@@ -325,7 +326,8 @@ mcc::WarmCtx warm_ctx(mcc_problem* p) {
     const int copy_prev = (p->comm || p->peer_on) ? 1 : 0;   // sharded: k_solve copies the summed system
     return mcc::WarmCtx{p->sinv, reinterpret_cast<int*>(p->wsync + 3), p->prev2, p->prev_stride, copy_prev, p->wsync, p->warm_stats.p,
                         p->warm_poison, p->warm_wait_ticks, p->warm_idle_ticks, p->warm_delay_ticks,
-                        p->helper_refine && !copy_prev ? 1 : 0, p->xsol, p->helper_early};
+                        p->helper_refine && !copy_prev ? 1 : 0, p->xsol, p->helper_early,
+                        p->stamps.p ? p->stamps.p + p->stamps.n - 64 : nullptr, p->inv_la};
 }
 
 mcc::PeerCtx peer_ctx(mcc_problem* p, bool on) {
@@ -1244,6 +1246,8 @@ int mcc_create(mcc_problem** out, const mcc_desc* d) {
     if (const char* f = std::getenv("MCC_HELPER_REFINE")) p->helper_refine = p->helper_refine && std::atoi(f) != 0;
     p->helper_early = p->helper_refine && !p->use_group;
     if (const char* f = std::getenv("MCC_HELPER_POLL")) p->helper_early = p->helper_refine && std::atoi(f) != 0;
+    p->inv_la = p->use_group;   // (mcc_kernels.hip gj_inverse_blocked: where the helper's cycle bounds the step)
+    if (const char* f = std::getenv("MCC_INV_LA")) p->inv_la = std::atoi(f) != 0;
     if (const char* f = std::getenv("MCC_WARM_POISON")) p->warm_poison = std::atoi(f);
     if (const char* f = std::getenv("MCC_WARM_TIMEOUT_MS")) p->warm_wait_ticks = (long long)(std::max(1.0, std::atof(f)) * 1e5);
     if (const char* f = std::getenv("MCC_WARM_DELAY_US")) p->warm_delay_ticks = (long long)(std::max(0.0, std::atof(f)) * 1e2);
@@ -1605,9 +1609,10 @@ int mcc_debug_stamps(mcc_problem* p, long long* out, int n) {
     if (!p || !out) return fail(MCC_EINVAL, "null argument");
     HIPCHK(hipSetDevice(p->device));
     if (!p->stamps.p) {
-        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + mcc::kSchurStampStride * (size_t)(p->n_items + p->n_norm_chunks) + 16;
+        const size_t n_st = mcc::kStampStride * (size_t)std::max(p->V, 1) + mcc::kSchurStampStride * (size_t)(p->n_items + p->n_norm_chunks) + 16 + 64;   // (+ the helper's)
         HIPCHK(p->stamps.alloc(n_st));
         HIPCHK(hipMemset(p->stamps.p, 0, sizeof(long long) * n_st));
+        HIPCHK(hipMemset(p->stamps.p + n_st - 64, 0xFF, sizeof(long long) * 64));   // the helper's: -1 until written
         drop_graphs(p);   // graphs captured the old pointer
         return MCC_OK;   // armed: the next steps record
     }

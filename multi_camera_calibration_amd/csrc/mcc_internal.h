@@ -326,6 +326,8 @@ struct WarmCtx {
     double* xsol;            // refine: [kWarmN] uncached, the helper's solution of the published system
     int poll;                // refine: k_schur publishes at its start and the helper polls prev2's words
                              // (SchurArgs::wpub_early), else one batch once the system is complete
+    long long* hst;          // MCC_DIAG builds: the helper's phase stamps, [4 systems][16] (null otherwise)
+    int inv_la;              // the helper inverts with the look-ahead schedule (gj_inverse_blocked<true>)
 };
 constexpr int kWarmMaxIters = 4;
 

@@ -2893,7 +2893,7 @@ __host__ __device__ __forceinline__ int warm_lc2(int m) { return (m * (m + 1) / 
 // the solution and warm_refine's work area
 __host__ __device__ __forceinline__ size_t helper_shmem_doubles(int m, bool refine) {
     const size_t M = 16 * (size_t)((m + 15) / 16);
-    return M * (M + 1) + 16 * kBlkLd + (refine ? 2 * (size_t)warm_lc2(m) + 2 * kWarmN + 8 : 0);
+    return M * (M + 1) + 16 * kBlkLd + (refine ? 2 * (size_t)warm_lc2(m) + 2 * kWarmN + 8 : 16 * kBlkLd);
 }
 // LDS doubles of the warm path behind x (kWarmN): packed [S | r] (even length), S^-1 (M x (M + 2)),
 // the residual (kWarmN), wave maxima
@@ -3194,39 +3194,96 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
 }
 
 // In-place blocked Gauss-Jordan inverse of the padded SPD system in LDS (A: M x M, stride ld = M + 1,
-// 16 x 16 blocks; the helper).  Per pivot block kb: P^-1 (wave 0, gjb_inverse16); the pivot block row
+// 16 x 16 blocks; the helper).  Per pivot block kb: P^-1 (gjb_inverse16); the pivot block row
 // A[kb][j] <- P^-1 A[kb][j]; every other block A[i][j] -= A[i][kb] A[kb][j]; the pivot block column
-// A[i][kb] <- -A[i][kb] P^-1 and A[kb][kb] <- P^-1.  Off the critical path (the step's linearisation
-// runs meanwhile), so no look-ahead.  Returns false (every thread) if a pivot is not > 0.
-__device__ bool gj_inverse_blocked(double* A, double* PV, int M) {
+// A[i][kb] <- -A[i][kb] P^-1 and A[kb][kb] <- P^-1.  Scheduled with a look-ahead (round 6): in kb's
+// block update wave 0 takes the next pivot block (kb + 1, kb + 1) first and inverts it while the
+// other waves update the rest, and the pivot column of kb shares one phase with the pivot row of
+// kb + 1 (block (kb + 1, kb) goes through both, in that order, on one wave) -- two barriers per pivot
+// block instead of four, and the serial 16 x 16 inverse (1.65 us of the 4.9 us per block) off the
+// critical path except its own chain.  The same products in the same order: bitwise the round-5
+// schedule's inverse.  m = 90: 29.1 -> 19.1 us alone on a CU (tools/inv_bench.hip).  PV0, PV1: the
+// 16 x kBlkLd scratch of the even and odd pivot blocks.  Returns false (every thread) if a pivot is not > 0.
+// LA = false: the round-5 schedule (four phases per pivot block, PV0 only).  WarmCtx::inv_la picks:
+// the look-ahead where the helper's cycle bounds the step (k_group's short steps: the config3 x8 shard
+// 45.0 -> 41.1 us), round 5's where the inversion overlaps a long linearisation -- there the denser
+// look-ahead slowed the co-resident linearisation workgroups (config3 107.8 -> 109.3 us per step).
+template <bool LA>
+__device__ bool gj_inverse_blocked(double* A, double* PV0, double* PV1, int M) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-    const int nb = M / 16, ld = M + 1;
+    const int nb = M / 16, n1 = nb - 1, ld = M + 1;
     __shared__ int bad_s;
     if (tid == 0) bad_s = 0;
-    for (int kb = 0; kb < nb; ++kb) {
-        if (wave == 0 && !gjb_inverse16(A + 16 * kb * ld + 16 * kb, ld, PV, lane) && lane == 0) bad_s = 1;
-        __syncthreads();
-        for (int it = wave; it < nb - 1; it += nw) {   // pivot block row
-            const int jb = it < kb ? it : it + 1;
-            double* C = A + 16 * kb * ld + 16 * jb;
-            blk_mfma(C, ld, PV, kBlkLd, C, ld, false, true);
-        }
-        __syncthreads();
-        for (int it = wave; it < (nb - 1) * (nb - 1); it += nw) {   // the other blocks
-            const int r = it / (nb - 1), c = it % (nb - 1);
-            const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
-            blk_mfma(A + 16 * ib * ld + 16 * jb, ld, A + 16 * ib * ld + 16 * kb, ld, A + 16 * kb * ld + 16 * jb, ld,
-                     true, false);
-        }
-        __syncthreads();
-        for (int it = wave; it < nb; it += nw) {   // the pivot block column, and the pivot block
-            double* C = A + 16 * it * ld + 16 * kb;
-            if (it != kb) {
-                blk_mfma(C, ld, C, ld, PV, kBlkLd, true, true);
-            } else {
-                const int i = lane & 15, g = lane >> 4;
+    auto blk = [&](int ib, int jb) { return A + 16 * ib * ld + 16 * jb; };
+    auto pvb = [&](int kb) { return kb & 1 ? PV1 : PV0; };
+    if (!LA) {
+        for (int kb = 0; kb < nb; ++kb) {
+            if (wave == 0 && !gjb_inverse16(blk(kb, kb), ld, PV0, lane) && lane == 0) bad_s = 1;
+            __syncthreads();
+            for (int it = wave; it < n1; it += nw) {   // pivot block row
+                double* C = blk(kb, it < kb ? it : it + 1);
+                blk_mfma(C, ld, PV0, kBlkLd, C, ld, false, true);
+            }
+            __syncthreads();
+            for (int it = wave; it < n1 * n1; it += nw) {   // the other blocks
+                const int r = it / n1, c = it % n1;
+                const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
+                blk_mfma(blk(ib, jb), ld, blk(ib, kb), ld, blk(kb, jb), ld, true, false);
+            }
+            __syncthreads();
+            for (int it = wave; it < nb; it += nw) {   // the pivot block column, and the pivot block
+                double* C = blk(it, kb);
+                if (it != kb) {
+                    blk_mfma(C, ld, C, ld, PV0, kBlkLd, true, true);
+                } else {
+                    const int i = lane & 15, g = lane >> 4;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) C[i * ld + 4 * g + c] = PV[i * kBlkLd + 4 * g + c];
+                    for (int c = 0; c < 4; ++c) C[i * ld + 4 * g + c] = PV0[i * kBlkLd + 4 * g + c];
+                }
+            }
+            __syncthreads();
+        }
+        return bad_s == 0;
+    }
+    // kb = -1: the first pivot block's inverse, then its pivot block row
+    for (int kb = -1; kb < nb; ++kb) {
+        const bool next = kb + 1 < nb;
+        if (next && wave == 0) {   // the next pivot block first, then its inverse
+            if (kb >= 0) blk_mfma(blk(kb + 1, kb + 1), ld, blk(kb + 1, kb), ld, blk(kb, kb + 1), ld, true, false);
+            if (!gjb_inverse16(blk(kb + 1, kb + 1), ld, pvb(kb + 1), lane) && lane == 0) bad_s = 1;
+        } else if (kb >= 0) {
+            const int w0 = next ? wave - 1 : wave, nws = next ? nw - 1 : nw;
+            const int skip = next ? kb * n1 + kb : n1 * n1;   // (kb + 1, kb + 1): wave 0's
+            for (int it = w0; it < n1 * n1 - (next ? 1 : 0); it += nws) {
+                const int t = it < skip ? it : it + 1;
+                const int r = t / n1, c = t % n1;
+                const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
+                blk_mfma(blk(ib, jb), ld, blk(ib, kb), ld, blk(kb, jb), ld, true, false);
+            }
+        }
+        __syncthreads();
+        // items < ncol: the pivot block column of kb (item kb + 1, dealt first, also takes its block
+        // through the pivot row of kb + 1); the rest: that row's other blocks (columns other than kb, kb + 1)
+        const int ncol = kb >= 0 ? nb : 0;
+        const int nrow = next ? (kb >= 0 ? nb - 2 : nb - 1) : 0;
+        for (int it0 = wave; it0 < ncol + nrow; it0 += nw) {
+            if (it0 < ncol) {
+                const int it = next && it0 <= kb + 1 ? (it0 == 0 ? kb + 1 : it0 - 1) : it0;
+                double* C = blk(it, kb);
+                if (it != kb) {
+                    blk_mfma(C, ld, C, ld, pvb(kb), kBlkLd, true, true);
+                    if (it == kb + 1) blk_mfma(C, ld, pvb(kb + 1), kBlkLd, C, ld, false, true);
+                } else {
+                    const int i = lane & 15, g = lane >> 4;
+                    const double* P = pvb(kb);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) C[i * ld + 4 * g + c] = P[i * kBlkLd + 4 * g + c];
+                }
+            } else {
+                const int q = it0 - ncol;
+                const int jb = kb < 0 ? q + 1 : (q < kb ? q : q + 2);
+                double* C = blk(kb + 1, jb);
+                blk_mfma(C, ld, pvb(kb + 1), kBlkLd, C, ld, false, true);
             }
         }
         __syncthreads();
@@ -3250,6 +3307,9 @@ __device__ bool gj_inverse_blocked(double* A, double* PV, int M) {
 // (tools/diag_solve.py), which now run while k_schur ends and k_solve starts.  The refinement runs
 // only with the inverse of system e - 1 (a batch's helper starts from sinv and the epoch sync[1]
 // names), so its branch is a function of the systems alone, as before.
+// LA: the look-ahead inversion (WarmCtx::inv_la; a template, as both schedules inlined into one kernel
+// spilled it)
+template <bool LA>
 __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m, int n_systems) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     __shared__ unsigned ep_s;
@@ -3307,6 +3367,14 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
             return;
         }
         const unsigned e = ep_s;
+#ifdef MCC_DIAG   // (the helper's phases: seen, staged, S gathered, refined, x published, inverted; [6] the
+                  // corrections, [7] the epoch; [15] stays -1, the host's marker)
+#define HSTAMP(k) do { if (tid == 0 && w.hst) w.hst[(e & 3u) * 16 + (k)] = (long long)MCC_DIAG_CLOCK(); } while (0)
+        if (tid == 0 && w.hst) w.hst[(e & 3u) * 16 + 7] = e;
+#else
+#define HSTAMP(k) do { } while (0)
+#endif
+        HSTAMP(0);
         // system e (solved by the update step whose iteration counter was e - 1: k_schur wrote it to
         // prev2[(e - 1) & 1]) -> the full symmetric matrix in LDS (padding: identity)
         const int ntri = m * (m + 1) / 2;
@@ -3372,6 +3440,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
                     __builtin_amdgcn_s_sleep(1);
                 }
             }
+            HSTAMP(1);
             int status = 0, corr = 0;
 #ifdef MCC_HELPER_RELOAD   // (A/B debug builds only)
             if (have_s && held == e - 1u) {
@@ -3393,9 +3462,14 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
                 double* xso = Pko + 2 * warm_lc2(mo);
                 double Sr[kWarmQ];
                 warm_gather_s(Pko, mo, Sr);
+                HSTAMP(2);
                 const bool conv = warm_refine<true>(Sr, Ao, ldo, Pko, xso, xso + kWarmN, mo, nullptr, &corr);
                 status = conv && !w.poison ? 1 : 2;   // (test: a poisoned helper's solves all fall back)
             }
+            HSTAMP(3);
+#ifdef MCC_DIAG
+            if (tid == 0 && w.hst) w.hst[(e & 3u) * 16 + 6] = corr;
+#endif
             if (status == 1)
                 for (int t = tid; t < m; t += blockDim.x)
                     __hip_atomic_store(reinterpret_cast<unsigned long long*>(w.xsol + t), (unsigned long long)__double_as_longlong(xs[t]),
@@ -3412,6 +3486,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_sys_u32(w.sync + 4, e);
             }
+            HSTAMP(4);
             // (the words go back to kFoldEmpty in the next step's k_schur, schur_block_store: 33 KB of
             // stores here lengthened the helper's cycle, which bounds the 8-rank shard's step)
             for (int t = tid; t < ntri; t += blockDim.x) {
@@ -3435,7 +3510,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
             if (i >= m || j >= m) A[i * ld + j] = i == j ? 1.0 : 0.0;
         }
         __syncthreads();
-        const bool ok = gj_inverse_blocked(A, PV, M);
+        // (the odd pivot blocks' scratch: refine, the staged system, copied into A by now; else its own)
+        const bool ok = gj_inverse_blocked<LA>(A, PV, PV + 16 * kBlkLd, M);
+        HSTAMP(5);
+#undef HSTAMP
 #ifdef MCC_HELPER_RELOAD
         dump_inverse();
 #else
@@ -4669,7 +4747,8 @@ hipError_t mcc_attrs_solve(size_t ss) {
     hipError_t err = hipSuccess;
     for (hipError_t e : {hipFuncSetAttribute((const void*)&k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss),
                          hipFuncSetAttribute((const void*)&k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss),
-                         hipFuncSetAttribute((const void*)&k_sinv_helper, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss)})
+                         hipFuncSetAttribute((const void*)&k_sinv_helper<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss),
+                         hipFuncSetAttribute((const void*)&k_sinv_helper<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ss)})
         if (e != hipSuccess) err = e;
     return err;
 }
@@ -4696,7 +4775,10 @@ hipError_t mcc_launch_debug_solve(const double* packed, double* x, int m, int* e
 }
 hipError_t mcc_launch_sinv_helper(const WarmCtx& w, int m, int n_systems, hipStream_t s) {
     const size_t shm = helper_shmem_doubles(m, w.refine != 0) * sizeof(double);
-    hipLaunchKernelGGL(k_sinv_helper, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
+    if (w.inv_la)
+        hipLaunchKernelGGL(k_sinv_helper<true>, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
+    else
+        hipLaunchKernelGGL(k_sinv_helper<false>, dim3(1), dim3(kSolveThreads), shm, s, w, m, n_systems);
     return hipGetLastError();
 }
 #endif  // MCC_IN(5)

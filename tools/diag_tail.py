@@ -32,13 +32,18 @@ print(f"{cfg} shard 1/{shard}: {p.n_photos} views, {p.n_edges} edges, path {ba.s
 ba.set_params(p.x0)
 ba.step(40)
 ba.synchronize()
+steps_per_rep = int(os.environ.get("TAIL_STEPS", "1"))   # > 1: the last of a batch (a resident helper's steady state)
 ba.stamps()   # arm
 nv = max(p.n_photos, 1)
 out = []
 for r in range(reps):
-    ba.step(1)
+    ba.step(steps_per_rep)
     ba.synchronize()
     raw = ba.stamps().reshape(-1).astype(np.int64)
+    # the helper's [4 systems][16] at the buffer's end (-1 until written; slot 15 never is)
+    hb = int(np.nonzero(raw == -1)[0].max()) - 63
+    hst = raw[hb:hb + 64].reshape(4, 16).copy()
+    raw[hb:] = 0
     ph = raw[:32 * nv].reshape(nv, 32)
     g0 = ph[:, 0][ph[:, 0] > 0]
     ge = ph[:, 10][ph[:, 10] > 0]
@@ -58,6 +63,16 @@ for r in range(reps):
            "solve_entry": us(ks[0]), "solve_loads": us(ks[4]) if ks[4] else float("nan"),
            "solve_x_in": us(ks[11]) if ks[11] else float("nan"), "solve_done": us(ks[5]) if ks[5] else float("nan"),
            "camera_update": us(ks[6]) if ks[6] else float("nan")}
+    # the helper: this step's system (the largest epoch) seen, staged, refined, x published; the
+    # previous system's inversion end
+    cur = int(np.argmax(hst[:, 7]))
+    e = int(hst[cur, 7])
+    prv = [i for i in range(4) if hst[i, 7] == e - 1]
+    for k, name in enumerate(("helper_seen", "helper_staged", "helper_gathered", "helper_refined", "helper_x_published")):
+        row[name] = us(hst[cur, k]) if hst[cur, k] > 0 else float("nan")
+    row["helper_prev_inverted"] = us(hst[prv[0], 5]) if prv and hst[prv[0], 5] > 0 else float("nan")
+    row["helper_inverted"] = us(hst[cur, 5]) if hst[cur, 5] > 0 else float("nan")
+    row["helper_corrections"] = float(hst[cur, 6])
     out.append(row)
 ba.close()
 keys = list(out[0])
