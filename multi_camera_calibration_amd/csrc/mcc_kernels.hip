@@ -3202,7 +3202,8 @@ __device__ void warm_finish(const double* packed, const WarmCtx& w, double* x, i
 // kb + 1 (block (kb + 1, kb) goes through both, in that order, on one wave) -- two barriers per pivot
 // block instead of four, and the serial 16 x 16 inverse (1.65 us of the 4.9 us per block) off the
 // critical path except its own chain.  The same products in the same order: bitwise the round-5
-// schedule's inverse.  m = 90: 29.1 -> 19.1 us alone on a CU (tools/inv_bench.hip).  PV0, PV1: the
+// schedule's inverse.  m = 90: 29.1 -> 22.8 us alone on a CU (tools/inv_bench.hip; 19.1 with the first
+// pivot block as a separate prologue, which spilled the helper).  PV0, PV1: the
 // 16 x kBlkLd scratch of the even and odd pivot blocks.  Returns false (every thread) if a pivot is not > 0.
 // LA = false: the round-5 schedule (four phases per pivot block, PV0 only).  WarmCtx::inv_la picks:
 // the look-ahead where the helper's cycle bounds the step (k_group's short steps: the config3 x8 shard

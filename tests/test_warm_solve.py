@@ -14,7 +14,8 @@ it replaces is the reference's sparse CG on the whole normal equations
     optimisation does not depend on the problem's earlier ones (each starts without an inverse);
   * a NaN inverse (MCC_WARM_POISON=1) makes every warm solve fall back, and the fallback is the
     direct elimination: bitwise the MCC_WARM=0 result;
-  * m = 126 (beyond the staged warm path's M <= 96) runs the direct elimination only.
+  * m = 126 (beyond the staged warm path's M <= 96) runs the direct elimination only;
+  * the helper's look-ahead inversion (round 6) is bitwise the round-5 schedule's.
 """
 import os
 import sys
@@ -160,6 +161,36 @@ def test_helper_refinement_is_bitwise_k_solves(name, poll):
     out = []
     for env in ({"MCC_HELPER_REFINE": "0"}, {"MCC_HELPER_POLL": poll}):
         ba = make(p, env)
+        try:
+            x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
+            ba.set_params(p.x0)
+            ba.step(24)
+            ba.check()
+            xs = ba.get_params()
+            st = ba.solve_stats()
+        finally:
+            ba.close()
+        out.append((x, it, xs, st))
+    (x0, it0, xs0, st0), (x1, it1, xs1, st1) = out
+    assert it0 == it1
+    assert np.array_equal(x0, x1) and np.array_equal(xs0, xs1)
+    for k in ("warm", "corrections", "fallbacks", "direct"):
+        assert st0[k] == st1[k], (st0, st1)
+    assert st1["warm"] > 0
+
+
+@pytest.mark.parametrize("name", ["config3_small", "m48"])
+@pytest.mark.parametrize("refine", ["0", "1"])
+def test_lookahead_inverse_is_bitwise_the_round5_schedule(name, refine):
+    """The helper's inverse with the look-ahead schedule (gj_inverse_blocked<true>, the k_group path's
+    default) is bitwise the round-5 schedule's (MCC_INV_LA=0): the same products in the same order.
+    Checked through everything the inverse feeds -- the optimize, the free-running steps and the solve
+    statistics -- with the helper refining (refine = 1) and with k_solve refining from the inverse the
+    helper stores (0)."""
+    p = CASES[name]()
+    out = []
+    for la in ("0", "1"):
+        ba = make(p, {"MCC_INV_LA": la, "MCC_HELPER_REFINE": refine})
         try:
             x, m, it, _ = ba.optimize_extrinsics(p.x0, crit_type=3, max_count=200, eps=1e-7)
             ba.set_params(p.x0)

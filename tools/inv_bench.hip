@@ -4,7 +4,9 @@
 // One workgroup of kSolveThreads inverts a random SPD system REPS times (S reloaded into LDS each
 // time); prints the median s_memrealtime time per inversion (us), max |S S^-1 - I| and a hash of
 // the inverse's bits (bitwise A/B of variants).  Second argument: 0 round 5's schedule, 1 the same with
-// its phases timed, 2 the look-ahead (gj_inverse_blocked<true>).  (Row strides M + 2, + 3, + 5 instead
+// its phases timed, 2 the look-ahead (gj_inverse_blocked<true>), 3 the look-ahead with its first pivot
+// block as a separate prologue (19.1 vs 22.7 us at m = 90: faster alone, but inlined into the helper
+// it spilled, and with the helper's refinement indices made opaque to stop that, the shard lost 0.7 us).  (Row strides M + 2, + 3, + 5 instead
 // of M + 1 measured the same, 19.4-19.7 us at m = 90.)
 #include "../multi_camera_calibration_amd/csrc/mcc_kernels.hip"
 
@@ -66,6 +68,70 @@ __device__ bool inv_phased(double* A, double* PV, int M, long long* ph) {
     return bad_s == 0;
 }
 
+// (A/B) the look-ahead with its kb = -1 step as a separate prologue
+__device__ bool inv_lookahead_prologue(double* A, double* PV, int M) {
+    using namespace mcc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+    const int nb = M / 16, ld = M + 1, n1 = nb - 1;
+    __shared__ int bad_s;
+    if (tid == 0) bad_s = 0;
+    auto blk = [&](int ib, int jb) { return A + 16 * ib * ld + 16 * jb; };
+    auto pvb = [&](int kb) { return PV + (kb & 1) * 16 * kBlkLd; };
+    if (wave == 0 && !gjb_inverse16(blk(0, 0), ld, pvb(0), lane) && lane == 0) bad_s = 1;
+    __syncthreads();
+    for (int it = wave; it < nb - 1; it += nw) {
+        double* C = blk(0, it + 1);
+        blk_mfma(C, ld, pvb(0), kBlkLd, C, ld, false, true);
+    }
+    __syncthreads();
+    for (int kb = 0; kb < nb; ++kb) {
+        if (kb + 1 < nb) {
+            if (wave == 0) {
+                blk_mfma(blk(kb + 1, kb + 1), ld, blk(kb + 1, kb), ld, blk(kb, kb + 1), ld, true, false);
+                if (!gjb_inverse16(blk(kb + 1, kb + 1), ld, pvb(kb + 1), lane) && lane == 0) bad_s = 1;
+            } else {
+                for (int it = wave - 1; it < n1 * n1 - 1; it += nw - 1) {
+                    const int t = it < kb * n1 + kb ? it : it + 1;
+                    const int r = t / n1, c = t % n1;
+                    const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
+                    blk_mfma(blk(ib, jb), ld, blk(ib, kb), ld, blk(kb, jb), ld, true, false);
+                }
+            }
+        } else {
+            for (int it = wave; it < n1 * n1; it += nw) {
+                const int r = it / n1, c = it % n1;
+                const int ib = r < kb ? r : r + 1, jb = c < kb ? c : c + 1;
+                blk_mfma(blk(ib, jb), ld, blk(ib, kb), ld, blk(kb, jb), ld, true, false);
+            }
+        }
+        __syncthreads();
+        const bool next = kb + 1 < nb;
+        const int nrow = next ? nb - 2 : 0;
+        for (int it0 = wave; it0 < nb + nrow; it0 += nw) {
+            const int it = next && it0 <= kb + 1 ? (it0 == 0 ? kb + 1 : it0 - 1) : it0;
+            if (it < nb) {
+                double* C = blk(it, kb);
+                if (it != kb) {
+                    blk_mfma(C, ld, C, ld, pvb(kb), kBlkLd, true, true);
+                    if (it == kb + 1) blk_mfma(C, ld, pvb(kb + 1), kBlkLd, C, ld, false, true);
+                } else {
+                    const int i = lane & 15, g = lane >> 4;
+                    const double* P = pvb(kb);
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) C[i * ld + 4 * g + c] = P[i * kBlkLd + 4 * g + c];
+                }
+            } else {
+                const int q = it - nb;
+                const int jb = q < kb ? q : q + 2;
+                double* C = blk(kb + 1, jb);
+                blk_mfma(C, ld, pvb(kb + 1), kBlkLd, C, ld, false, true);
+            }
+        }
+        __syncthreads();
+    }
+    return bad_s == 0;
+}
+
 __global__ __launch_bounds__(mcc::kSolveThreads) void k_inv_bench(const double* Sg, int m, double* out, long long* ticks, int* ok, long long* ph, int phased) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int tid = threadIdx.x, M = 16 * ((m + 15) / 16);
@@ -81,7 +147,7 @@ __global__ __launch_bounds__(mcc::kSolveThreads) void k_inv_bench(const double* 
         __syncthreads();
         long long t0 = 0, c0 = 0;
         if (tid == 0) { t0 = (long long)__builtin_amdgcn_s_memrealtime(); c0 = (long long)__builtin_amdgcn_s_memtime(); }
-        good &= phased == 1 ? inv_phased(A, PV, M, ph) : phased == 2 ? mcc::gj_inverse_blocked<true>(A, PV, PV + 16 * mcc::kBlkLd, M) : mcc::gj_inverse_blocked<false>(A, PV, PV + 16 * mcc::kBlkLd, M);
+        good &= phased == 1 ? inv_phased(A, PV, M, ph) : phased == 2 ? mcc::gj_inverse_blocked<true>(A, PV, PV + 16 * mcc::kBlkLd, M) : phased == 3 ? inv_lookahead_prologue(A, PV, M) : mcc::gj_inverse_blocked<false>(A, PV, PV + 16 * mcc::kBlkLd, M);
         __syncthreads();
         if (tid == 0) {
             ticks[rep] = (long long)__builtin_amdgcn_s_memrealtime() - t0;
