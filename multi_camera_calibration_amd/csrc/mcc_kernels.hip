@@ -3014,6 +3014,13 @@ __device__ __forceinline__ void ld_nc_x2_5(const double* p0, const double* p1, c
         : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4)
         : "memory");
 }
+// 16 bytes of epoch words past every cache, waited for (k_solve's poll of the helper's {epoch, status,
+// corrections}: one request, so the status words written before the epoch arrive with it)
+__device__ __forceinline__ uint4 ld_nc_u32x4(const unsigned* p) {
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+    return v;
+}
 __device__ __forceinline__ void st_sys_x2(double* p, double a, double b) {
     f64x2_t v;
     v.x = a;
@@ -3071,16 +3078,16 @@ __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigne
         // the helper solves: wait for its solution of the system k_schur published (epoch e); 2: use
         // it, 0: eliminate (no inverse of the previous system, or the refinement did not converge)
         const unsigned e = ld_sys_u32(w.sync);
-        uint4 hy = *reinterpret_cast<const uint4*>(w.sync + 4);   // {solved epoch, status, corrections, -}
+        // {solved epoch, status, corrections, -} in one 16-byte load per poll (round 6: the status words
+        // were re-read after the epoch matched, one more memory round trip on every waited step)
+        uint4 hy = ld_nc_u32x4(w.sync + 4);
         if (hy.x != e) {
             w.stats[4] += 1;
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             while (hy.x != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < w.wait_ticks) {
                 __builtin_amdgcn_s_sleep(2);
-                hy.x = ld_sys_u32(w.sync + 4);
+                hy = ld_nc_u32x4(w.sync + 4);
             }
-            hy.y = ld_sys_u32(w.sync + 5);
-            hy.z = ld_sys_u32(w.sync + 6);
         }
         // use: -1 the helper did not deliver; else (corrections << 3) | (0 no inverse, 1 refined, not
         // converged, 2 converged: x is the helper's); counted by warm_finish, when the solve is used
