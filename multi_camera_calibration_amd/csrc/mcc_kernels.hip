@@ -3095,22 +3095,21 @@ __device__ __forceinline__ void warm_check(const WarmCtx& w, int* use_s, unsigne
         *e_s = e;
         return;
     }
-    const uint4 sy = *reinterpret_cast<const uint4*>(w.sync);   // {published, inverted, stop, PD}
+    uint4 sy = ld_nc_u32x4(w.sync);   // {published, inverted, stop, PD}: as above, one load per poll
     const unsigned e = sy.x;
-    unsigned h = sy.y, ok = sy.w;
     int use = 0;
     if (e == 0) {
         w.stats[3] += 1;
     } else {
-        if (h != e) {
+        if (sy.y != e) {
             w.stats[4] += 1;   // waited for the helper (the branch taken below does not depend on it)
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            while (h != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < w.wait_ticks) {
+            while (sy.y != e && (long long)__builtin_amdgcn_s_memrealtime() - t0 < w.wait_ticks) {
                 __builtin_amdgcn_s_sleep(2);
-                h = ld_sys_u32(w.sync + 1);
+                sy = ld_nc_u32x4(w.sync);
             }
-            ok = ld_sys_u32(w.sync + 3);
         }
+        const unsigned h = sy.y, ok = sy.w;
         use = h != e ? -1 : ok ? 1 : 0;
         if (use == 0) w.stats[3] += 1;
     }
