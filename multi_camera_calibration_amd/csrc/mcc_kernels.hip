@@ -3481,18 +3481,18 @@ __global__ __launch_bounds__(kSolveThreads) void k_sinv_helper(WarmCtx w, int m,
                 for (int t = tid; t < m; t += blockDim.x)
                     __hip_atomic_store(reinterpret_cast<unsigned long long*>(w.xsol + t), (unsigned long long)__double_as_longlong(xs[t]),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (tid == 0) {   // (with x: k_solve trusts them only once the epoch below matches, and the
+                              // previous system's k_solve has ended before this system was published)
+                st_sys_u32(w.sync + 5, (unsigned)status);
+                st_sys_u32(w.sync + 6, (unsigned)corr);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0 && w.delay_ticks > 0) {   // test: a slow helper (k_solve must wait, not switch)
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
                 while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < w.delay_ticks) __builtin_amdgcn_s_sleep(8);
             }
-            if (tid == 0) {
-                st_sys_u32(w.sync + 5, (unsigned)status);
-                st_sys_u32(w.sync + 6, (unsigned)corr);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_sys_u32(w.sync + 4, e);
-            }
+            if (tid == 0) st_sys_u32(w.sync + 4, e);
             HSTAMP(4);
             // (the words go back to kFoldEmpty in the next step's k_schur, schur_block_store: 33 KB of
             // stores here lengthened the helper's cycle, which bounds the 8-rank shard's step)
